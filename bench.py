@@ -1,0 +1,221 @@
+"""Benchmark: many-chain HMC on RosenbrockND, 64 dims, f32 (BASELINE.json
+configs[1]: 4096 chains per GPU; eps 0.01, L = 50, the reference's own
+high-dimensional Rosenbrock settings, hmc.rs:763-780).
+
+A "step" is one HMC transition of every chain (L leapfrogs each). The timed
+region runs --steps transitions with every state collected on the device,
+bracketed by a barrier and a device synchronize on both sides; the time is
+the maximum over ranks. Then the split-R-hat / ESS of the collected draws is
+computed on the GPUs (RCCL all-gather of per-split-chain summaries when N > 1).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Prints one JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
+VALU_F32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=100)
+    p.add_argument("--chains", type=int, default=4096, help="chains per GPU")
+    p.add_argument("--dim", type=int, default=64)
+    p.add_argument("--leapfrog", type=int, default=50)
+    p.add_argument("--eps", type=float, default=0.01)
+    p.add_argument("--dtype", default="f32", choices=["f32", "f64"])
+    p.add_argument("--layout", default="", help="lanes,elems override")
+    p.add_argument("--cpu-seconds", type=float, default=12.0,
+                   help="target CPU time of the oracle baseline sample (0 disables)")
+    p.add_argument("--cpu-threads", type=int, default=0)
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        # control plane only (barrier, RCCL unique-id broadcast): gloo on the
+        # host, so torch never initialises its own HIP runtime in this process.
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    import general_mcmc_amd as gm
+    from general_mcmc_amd import _lib
+
+    lib = _lib.load()
+    _lib.check(lib.gm_set_device(local))
+    lib = _lib.require_gpu()
+
+    dtype = np.float32 if a.dtype == "f32" else np.float64
+    s_bytes = np.dtype(dtype).itemsize
+    C_loc, D, L = a.chains, a.dim, a.leapfrog
+    C_glob = C_loc * world
+    offset = rank * C_loc
+    x0 = gm.init_with_seed(C_glob, D, 42, np.float64)[offset:offset + C_loc].astype(dtype)
+    sampler = gm.HMC(gm.RosenbrockND(), x0, a.eps, L, dtype=dtype, chain_offset=offset).set_seed(42)
+    if a.layout:
+        sampler.set_layout(*[int(v) for v in a.layout.split(",")])
+    lanes, elems = sampler.layout()
+
+    comm = None
+    if world > 1:
+        uid = (C.c_char * _lib.UNIQUE_ID_BYTES)()
+        if rank == 0:
+            _lib.check(lib.gm_comm_get_unique_id(uid))
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0)
+        uid = (C.c_char * _lib.UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
+        h = C.c_void_p()
+        _lib.check(lib.gm_comm_init(uid, world, rank, C.byref(h)))
+        comm = h
+
+    def barrier_sync():
+        _lib.check(lib.gm_device_synchronize())
+        if dist is not None:
+            dist.barrier()
+
+    # warmup = burn-in transitions (untimed)
+    if a.warmup > 0:
+        sampler.run_positions(0, a.warmup)
+    barrier_sync()
+    t0 = time.perf_counter()
+    ds = sampler.run_positions(a.steps, 0)
+    barrier_sync()
+    t_local = time.perf_counter() - t0
+    kernel_ms, launches = sampler.last_run_stats()
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([t_local, kernel_ms / max(launches, 1)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_max, launch_ms = float(t[0]), float(t[1])
+    else:
+        t_max, launch_ms = t_local, kernel_ms / max(launches, 1)
+
+    # diagnostics on the collected draws (device; RCCL all-gather when N > 1)
+    td0 = time.perf_counter()
+    if a.steps >= 4:
+        if comm is not None:
+            rhat = np.empty(D, dtype=np.float32)
+            ess = np.empty(D, dtype=np.float32)
+            _lib.check(lib.gm_split_rhat_ess_dist(comm, C.c_void_p(ds.ptr), _lib.dtype_code(dtype),
+                                                  C_loc, a.steps, D, D, C_loc * D, 1,
+                                                  _lib.ptr(rhat), _lib.ptr(ess)))
+        else:
+            rhat, ess = ds.split_rhat_ess()
+    else:
+        rhat = ess = np.full(D, np.nan, dtype=np.float32)
+    t_diag = time.perf_counter() - td0
+
+    # throughput: chain-leapfrogs per second over the whole job
+    value = C_glob * L * a.steps / t_max
+    # roofline of the dominant kernel: algorithmic bytes per launch (BASELINE.md
+    # "Roofline accounting"): per transition and chain
+    #   B_step = L (6D+1) s + (4D+2) s + D s (collected)
+    b_step = (L * (6 * D + 1) + (4 * D + 2) + D) * s_bytes
+    steps_per_launch = a.steps / max(launches, 1)
+    bytes_per_launch = b_step * C_loc * steps_per_launch
+    achieved_gbs = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+    flops_lf = 15 * (D - 1) + 6 * D  # RosenbrockND logp+grad and kick/drift/kick per chain-leapfrog
+    achieved_tflops = flops_lf * C_loc * L * steps_per_launch / (launch_ms * 1e-3) / 1e12
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            key = f"C{C_loc}_D{D}_L{L}_K{a.steps}_{a.dtype}"
+            if key in pm:
+                traffic = pm[key]["hbm_bytes_per_launch"]
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and a.cpu_seconds > 0:
+        cpu = cpu_baseline(gm, a, dtype, x0, lanes, elems)
+
+    if rank == 0:
+        line = {
+            "metric": "leapfrog steps/sec (whole node) + ESS/sec, 64-dim Rosenbrock HMC",
+            "value": value,
+            "unit": "chain-leapfrog steps/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": t_max * 1e3 / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": "synthetic (init: iid N(0,1) Philox seed 42; target RosenbrockND a=1 b=100)",
+            "config": {"workload": f"HMC RosenbrockND dim={D}, {C_loc} chains/GPU ({C_glob} total), "
+                                   f"eps={a.eps}, n_leapfrog={L}, all {a.steps} transitions collected",
+                       "chains_per_gpu": C_loc, "dim": D, "n_leapfrog": L, "step_size": a.eps,
+                       "layout": f"{lanes}x{elems}", "parallelism": f"chains sharded x{world}"},
+            "ess_per_sec": float(np.mean(ess)) / t_max,
+            "ess_min_per_sec": float(np.min(ess)) / t_max,
+            "ess": {"min": float(np.min(ess)), "mean": float(np.mean(ess))},
+            "rhat": {"min": float(np.min(rhat)), "max": float(np.max(rhat))},
+            "diag_seconds": t_diag,
+            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "hmc_kernel", "launch_ms": launch_ms,
+                         "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "valu": {"achieved_tflops": achieved_tflops,
+                                  "peak_tflops": VALU_F32_PEAK_TFLOPS,
+                                  "frac": achieved_tflops / VALU_F32_PEAK_TFLOPS}},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if comm is not None:
+        lib.gm_comm_destroy(comm)
+    sampler.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(gm, a, dtype, x0, lanes, elems):
+    """The CPU oracle (plain-C restatement of batched_hmc.rs, multithreaded over
+    chains like the reference's rayon par_iter) timed on a bounded sample of the
+    same workload: all chains, a few transitions."""
+    from tests import _oracle
+    ora = _oracle.load()
+    threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+    t = _oracle.Target(1, a.dim, a=1.0, b=100.0)
+    q = np.array(x0, copy=True)
+    t0 = time.perf_counter()
+    ora.hmc_run(t, q, a.eps, a.leapfrog, 42, 0, 1, 1, lanes, elems, threads=threads)
+    one = time.perf_counter() - t0
+    steps = max(1, int(a.cpu_seconds / max(one, 1e-6)))
+    t0 = time.perf_counter()
+    ora.hmc_run(t, q, a.eps, a.leapfrog, 42, 1, steps, steps, lanes, elems, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": x0.shape[0] * a.leapfrog * steps / dt, "unit": "chain-leapfrog steps/s",
+            "cores": threads, "kind": "port",
+            "sample": f"{x0.shape[0]} chains x {steps} transitions x {a.leapfrog} leapfrogs "
+                      f"(oracle/gm_oracle.c, {threads} threads, {dt:.1f}s)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+"""ctypes binding of libgmcmc.so (include/gmcmc.h).
+
+The product path has no CPU fallback: if the HIP library is missing, or no
+GPU is visible, every sampler raises instead of silently computing elsewhere.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GMCMC_LIB", os.path.join(_HERE, "lib", "libgmcmc.so"))
+
+GM_OK, GM_EINVAL, GM_EHIP, GM_ENOMEM, GM_ERCCL, GM_ESTATE = range(6)
+GM_F32, GM_F64 = 0, 1
+GM_TARGET_ROSENBROCK, GM_TARGET_ISO_GAUSS, GM_TARGET_GAUSS = 1, 2, 3
+UNIQUE_ID_BYTES = 128
+
+
+class GMError(RuntimeError):
+    """A non-zero status from libgmcmc (message from gm_last_error)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[gmcmc status {code}] {msg}")
+        self.code = code
+
+
+class gm_target(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("reserved", C.c_int32),
+        ("dim", C.c_int64),
+        ("a", C.c_double),
+        ("b", C.c_double),
+        ("std", C.c_double),
+        ("mean", C.POINTER(C.c_double)),
+        ("prec", C.POINTER(C.c_double)),
+        ("norm_const", C.c_double),
+    ]
+
+
+_vp = C.c_void_p
+_i64 = C.c_int64
+_i32 = C.c_int32
+_u64 = C.c_uint64
+_dbl = C.c_double
+_ip = C.c_int
+
+# name -> (restype, argtypes). Mirrors include/gmcmc.h one-to-one; the test
+# suite checks that every symbol the header declares is listed and exported.
+SIGNATURES = {
+    "gm_last_error": (C.c_char_p, []),
+    "gm_device_count": (_ip, [C.POINTER(C.c_int)]),
+    "gm_set_device": (_ip, [C.c_int]),
+    "gm_device_synchronize": (_ip, []),
+    "gm_gauss_from_cov": (_ip, [_i64, _vp, _vp, _vp]),
+    "gm_init_positions": (_ip, [_u64, _i64, _i64, _ip, _vp]),
+    "gm_target_logp_grad": (_ip, [C.POINTER(gm_target), _ip, _i64, _vp, _vp, _vp]),
+    "gm_hmc_create": (_ip, [C.POINTER(gm_target), _ip, _i64, _i64, _vp, _dbl, _i64, _i64, C.POINTER(_vp)]),
+    "gm_mh_create": (_ip, [C.POINTER(gm_target), _ip, _i64, _i64, _vp, _dbl, _i64, C.POINTER(_vp)]),
+    "gm_nuts_create": (_ip, [C.POINTER(gm_target), _ip, _i64, _i64, _vp, _dbl, _i32, _i64, C.POINTER(_vp)]),
+    "gm_set_seed": (_ip, [_vp, _u64]),
+    "gm_step": (_ip, [_vp]),
+    "gm_run": (_ip, [_vp, _i64, _i64, _vp]),
+    "gm_run_device": (_ip, [_vp, _i64, _i64, C.POINTER(_vp)]),
+    "gm_run_device_progress": (_ip, [_vp, _i64, _i64, C.POINTER(_vp)]),
+    "gm_run_progress": (_ip, [_vp, _i64, _i64, _vp, _vp, _vp]),
+    "gm_copy_samples": (_ip, [_vp, _vp]),
+    "gm_get_positions": (_ip, [_vp, _vp]),
+    "gm_set_positions": (_ip, [_vp, _vp]),
+    "gm_get_accept_counts": (_ip, [_vp, _vp]),
+    "gm_get_leapfrog_counts": (_ip, [_vp, _vp]),
+    "gm_nuts_get_step_size": (_ip, [_vp, _vp, _vp]),
+    "gm_sampler_layout": (_ip, [_vp, C.POINTER(_i32), C.POINTER(_i32)]),
+    "gm_sampler_set_layout": (_ip, [_vp, _i32, _i32]),
+    "gm_sampler_last_run_stats": (_ip, [_vp, C.POINTER(_dbl), C.POINTER(_i64)]),
+    "gm_sampler_set_steps_per_launch": (_ip, [_vp, _i64]),
+    "gm_destroy": (_ip, [_vp]),
+    "gm_split_rhat_ess": (_ip, [_vp, _ip, _i64, _i64, _i64, _vp, _vp]),
+    "gm_split_rhat_ess_device": (_ip, [_vp, _ip, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
+    "gm_comm_get_unique_id": (_ip, [_vp]),
+    "gm_comm_init": (_ip, [_vp, _i32, _i32, C.POINTER(_vp)]),
+    "gm_comm_destroy": (_ip, [_vp]),
+    "gm_split_rhat_ess_dist": (_ip, [_vp, _vp, _ip, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
+}
+
+_lib = None
+
+
+def load(path: str | None = None) -> C.CDLL:
+    """Load libgmcmc.so (raises if it is not built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise GMError(GM_ESTATE, f"{p} not found: build it with `make -C general-mcmc_amd` "
+                                 "(no CPU fallback exists)")
+    lib = C.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != GM_OK:
+        msg = load().gm_last_error()
+        raise GMError(rc, msg.decode() if msg else "")
+
+
+_gpu_checked = False
+
+
+def require_gpu() -> C.CDLL:
+    """The library, after checking that a HIP device is visible."""
+    global _gpu_checked
+    lib = load()
+    if not _gpu_checked:
+        n = C.c_int(0)
+        rc = lib.gm_device_count(C.byref(n))
+        if rc != GM_OK or n.value < 1:
+            raise GMError(GM_EHIP, "no HIP device visible: libgmcmc runs on MI355X (gfx950) only")
+        _gpu_checked = True
+    return lib
+
+
+def dtype_code(dtype) -> int:
+    dt = np.dtype(dtype)
+    if dt == np.float32:
+        return GM_F32
+    if dt == np.float64:
+        return GM_F64
+    raise ValueError(f"unsupported dtype {dt} (f32 or f64)")
+
+
+def np_dtype(code: int):
+    return np.float32 if code == GM_F32 else np.float64
+
+
+def ptr(a: np.ndarray) -> C.c_void_p:
+    return a.ctypes.data_as(C.c_void_p)

@@ -1,0 +1,151 @@
+"""Common plumbing for the sampler facades: a libgmcmc sampler handle."""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .stats import RunStats, split_rhat_mean_ess_device
+
+
+@dataclass
+class DeviceSamples:
+    """Samples left on the GPU by run_positions: [n_collect, n_chains, dim]
+    (batched_hmc.rs:115-123). Valid until the sampler's next run or close."""
+
+    ptr: int
+    n_collect: int
+    n_chains: int
+    dim: int
+    dtype: type
+    owner: "Sampler"
+
+    def to_host(self) -> np.ndarray:
+        return self.owner.copy_samples(self.n_collect)
+
+    def split_rhat_ess(self):
+        return split_rhat_mean_ess_device(self.ptr, self.dtype, self.n_chains, self.n_collect,
+                                          self.dim, (self.dim, self.n_chains * self.dim, 1))
+
+
+class Sampler:
+    _kind = ""
+
+    def __init__(self, create_fn, target, initial_positions, dtype, chain_offset, *extra):
+        x = np.asarray(initial_positions)
+        if x.ndim != 2:
+            raise ValueError("initial_positions must be [n_chains][dim]")
+        if dtype is None:
+            dtype = np.float64 if x.dtype == np.float64 else np.float32
+        self.dtype = np.dtype(dtype).type
+        x = np.ascontiguousarray(x, dtype=self.dtype)
+        self.n_chains, self.dim = x.shape
+        self._target = target
+        t, keep = target.to_struct(self.dim)
+        lib = _lib.require_gpu()
+        h = C.c_void_p()
+        _lib.check(create_fn(lib)(C.byref(t), _lib.dtype_code(self.dtype), self.n_chains, self.dim,
+                                  _lib.ptr(x), *extra, chain_offset, C.byref(h)))
+        del keep
+        self._h = h
+        self._lib = lib
+
+    # -- lifetime ---------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.gm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- common API -------------------------------------------------------
+    def _seed(self, seed: int):
+        _lib.check(self._lib.gm_set_seed(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF))
+        return self
+
+    def step(self):
+        _lib.check(self._lib.gm_step(self._h))
+
+    def run(self, n_collect: int, n_discard: int) -> np.ndarray:
+        """[n_chains, n_collect, dim] on the host."""
+        out = np.empty((self.n_chains, n_collect, self.dim), dtype=self.dtype)
+        _lib.check(self._lib.gm_run(self._h, n_collect, n_discard, _lib.ptr(out)))
+        return out
+
+    def run_positions(self, n_collect: int, n_discard: int) -> DeviceSamples:
+        p = C.c_void_p()
+        _lib.check(self._lib.gm_run_device(self._h, n_collect, n_discard, C.byref(p)))
+        return DeviceSamples(p.value or 0, n_collect, self.n_chains, self.dim, self.dtype, self)
+
+    def run_progress(self, n_collect: int, n_discard: int):
+        """(sample [n_chains, n_collect, dim], RunStats | None): the statistics
+        are the device-side split-R-hat/ESS of the collected draws."""
+        out = np.empty((self.n_chains, n_collect, self.dim), dtype=self.dtype)
+        if n_collect >= 2:
+            rhat = np.empty(self.dim, dtype=np.float32)
+            ess = np.empty(self.dim, dtype=np.float32)
+            _lib.check(self._lib.gm_run_progress(self._h, n_collect, n_discard, _lib.ptr(out),
+                                                 _lib.ptr(rhat), _lib.ptr(ess)))
+            return out, RunStats.from_arrays(rhat, ess)
+        _lib.check(self._lib.gm_run_progress(self._h, n_collect, n_discard, _lib.ptr(out), None, None))
+        return out, None
+
+    def copy_samples(self, n_collect: int) -> np.ndarray:
+        """Samples of the last run, [n_chains, n_collect, dim] on the host."""
+        out = np.empty((self.n_chains, n_collect, self.dim), dtype=self.dtype)
+        _lib.check(self._lib.gm_copy_samples(self._h, _lib.ptr(out)))
+        return out
+
+    def positions(self) -> np.ndarray:
+        out = np.empty((self.n_chains, self.dim), dtype=self.dtype)
+        _lib.check(self._lib.gm_get_positions(self._h, _lib.ptr(out)))
+        return out
+
+    def set_positions(self, x) -> None:
+        x = np.ascontiguousarray(np.asarray(x, dtype=self.dtype))
+        if x.shape != (self.n_chains, self.dim):
+            raise ValueError("positions must be [n_chains][dim]")
+        _lib.check(self._lib.gm_set_positions(self._h, _lib.ptr(x)))
+
+    def accept_counts(self) -> np.ndarray:
+        out = np.empty(self.n_chains, dtype=np.int64)
+        _lib.check(self._lib.gm_get_accept_counts(self._h, _lib.ptr(out)))
+        return out
+
+    def leapfrog_counts(self) -> np.ndarray:
+        out = np.empty(self.n_chains, dtype=np.int64)
+        _lib.check(self._lib.gm_get_leapfrog_counts(self._h, _lib.ptr(out)))
+        return out
+
+    def layout(self) -> tuple[int, int]:
+        a, b = C.c_int32(), C.c_int32()
+        _lib.check(self._lib.gm_sampler_layout(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def set_layout(self, lanes: int, elems: int):
+        _lib.check(self._lib.gm_sampler_set_layout(self._h, lanes, elems))
+        return self
+
+    def set_steps_per_launch(self, n: int):
+        _lib.check(self._lib.gm_sampler_set_steps_per_launch(self._h, n))
+        return self
+
+    def last_run_stats(self) -> tuple[float, int]:
+        ms, n = C.c_double(), C.c_int64()
+        _lib.check(self._lib.gm_sampler_last_run_stats(self._h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def target(self):
+        return self._target

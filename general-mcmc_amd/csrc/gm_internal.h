@@ -1,0 +1,79 @@
+// gm_internal.h — host-side declarations shared by the C ABI (gmcmc_api.cpp)
+// and the kernel translation units. Not part of the public boundary.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/gmcmc.h"
+
+namespace gm {
+
+void set_error(const std::string& msg);
+
+// Device-side view of a target (pointers are device memory).
+struct TargetDev {
+  int kind = 0;
+  int D = 0;
+  double a = 1, b = 100, std = 1, norm_const = 0;
+  const void* mu = nullptr;    // [D] of the sampler dtype
+  const void* prec = nullptr;  // [D*D] of the sampler dtype
+};
+
+struct Layout {
+  int lanes = 64;
+  int elems = 1;
+};
+bool layout_supported(int lanes, int elems);
+Layout default_layout(int D, gm_dtype dt, int kind);
+
+// ---- HMC -------------------------------------------------------------------
+struct HmcLaunch {
+  void* q = nullptr;            // [C*D] state, in/out
+  void* logp = nullptr;         // [C] out
+  long long* accepts = nullptr; // [C] in/out (+= accepted count)
+  void* samples = nullptr;      // [rows][C][D]
+  long long C = 0;
+  int D = 0;
+  double eps = 0;
+  int L = 0;
+  uint64_t seed = 0;
+  uint64_t step0 = 0;           // global transition index of the first step
+  uint32_t chain_offset = 0;
+  int n_steps = 0;
+  int collect_from = 0;         // steps s >= collect_from are stored ...
+  long long sample_row0 = 0;    // ... at row sample_row0 + (s - collect_from)
+};
+hipError_t launch_hmc(gm_dtype dt, const TargetDev& tg, const Layout& lay, const HmcLaunch& a,
+                      hipStream_t st);
+
+// ---- MH --------------------------------------------------------------------
+struct MhLaunch {
+  void* q = nullptr;
+  void* logp = nullptr;
+  long long* accepts = nullptr;
+  void* samples = nullptr;
+  long long C = 0;
+  int D = 0;
+  double prop_std = 1;
+  uint64_t seed = 0;
+  uint64_t step0 = 0;
+  uint32_t chain_offset = 0;
+  int n_steps = 0;
+  int collect_from = 0;
+  long long sample_row0 = 0;
+};
+hipError_t launch_mh(gm_dtype dt, const TargetDev& tg, const Layout& lay, const MhLaunch& a,
+                     hipStream_t st);
+
+// ---- target evaluation -----------------------------------------------------
+hipError_t launch_logp_grad(gm_dtype dt, const TargetDev& tg, const Layout& lay, long long n,
+                            const void* x, void* logp, void* grad, hipStream_t st);
+
+// ---- utilities -------------------------------------------------------------
+// [rows][C][D] -> [C][rows][D]
+hipError_t launch_transpose_samples(gm_dtype dt, const void* src, void* dst, long long rows,
+                                    long long C, long long D, hipStream_t st);
+
+}  // namespace gm

@@ -1,0 +1,76 @@
+// gm_layouts.h — the (lanes-per-chain, elements-per-lane) layouts compiled
+// into the sampling kernels, and a dispatcher from runtime values to template
+// instantiations.
+#pragma once
+#include "gm_device.h"
+#include "gm_internal.h"
+
+// X(LPC, E)
+#define GM_LAYOUT_LIST(X) \
+  X(1, 1)                 \
+  X(2, 1)                 \
+  X(4, 1)                 \
+  X(8, 1)                 \
+  X(16, 1)                \
+  X(32, 1)                \
+  X(64, 1)                \
+  X(16, 2)                \
+  X(32, 2)                \
+  X(64, 2)                \
+  X(8, 4)                 \
+  X(16, 4)                \
+  X(32, 4)                \
+  X(64, 4)                \
+  X(16, 8)                \
+  X(32, 8)                \
+  X(64, 8)                \
+  X(64, 16)
+
+namespace gm {
+
+template <class T, int LPC, int E, class F>
+hipError_t dispatch_target(const TargetDev& tg, F& f) {
+  switch (tg.kind) {
+    case GM_TARGET_ROSENBROCK: {
+      RosenbrockT<T> t;
+      t.a = (T)tg.a;
+      t.b = (T)tg.b;
+      t.b2 = (T)2 * (T)tg.b;
+      t.b4 = (T)4 * (T)tg.b;
+      t.D = tg.D;
+      return f.template operator()<T, LPC, E>(t);
+    }
+    case GM_TARGET_ISO_GAUSS: {
+      IsoGaussT<T> t;
+      t.var = (T)tg.std * (T)tg.std;
+      t.D = tg.D;
+      return f.template operator()<T, LPC, E>(t);
+    }
+    case GM_TARGET_GAUSS: {
+      GaussT<T> t;
+      t.mu = (const T*)tg.mu;
+      t.prec = (const T*)tg.prec;
+      t.nc = (T)tg.norm_const;
+      t.D = tg.D;
+      return f.template operator()<T, LPC, E>(t);
+    }
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+// Calls f.template operator()<T, LPC, E>(target) for the runtime
+// (dtype, target kind, layout); hipErrorInvalidValue when not compiled.
+template <class F>
+hipError_t dispatch(gm_dtype dt, const TargetDev& tg, const Layout& lay, F&& f) {
+#define GM_TRY_LAYOUT(L_, E_)                                       \
+  if (lay.lanes == L_ && lay.elems == E_) {                         \
+    if (dt == GM_F32) return dispatch_target<float, L_, E_>(tg, f); \
+    return dispatch_target<double, L_, E_>(tg, f);                  \
+  }
+  GM_LAYOUT_LIST(GM_TRY_LAYOUT)
+#undef GM_TRY_LAYOUT
+  return hipErrorInvalidValue;
+}
+
+}  // namespace gm

@@ -1,0 +1,40 @@
+// gm_nuts.h — host-side interface of the NUTS engine (nuts_kernels.hip).
+#pragma once
+#include <vector>
+
+#include "gm_internal.h"
+
+namespace gm {
+
+constexpr int NUTS_DEFAULT_MAX_DEPTH = 10;
+constexpr int NUTS_MAX_DEPTH_LIMIT = 30;
+
+struct NutsState {
+  bool inited = false;
+  int max_depth = 0;
+  void* eps = nullptr;      // [C] T   step size (generic_nuts.rs:573)
+  void* eps_bar = nullptr;  // [C] T   (:581)
+  void* h_bar = nullptr;    // [C] T   (:582)
+  void* mu = nullptr;       // [C] T   (:580)
+  void* stk_vec = nullptr;  // [max_depth][3][C][D] T : left-subtree first q, first p, proposal q
+  void* stk_alpha = nullptr;  // [max_depth][C*LPC] T
+  int* stk_n = nullptr;       // [max_depth][C*LPC]
+  int* stk_na = nullptr;      // [max_depth][C*LPC]
+  long long stk_lanes = 0;    // C*LPC the scalar stack was sized for
+  long long* n_leapfrog = nullptr;  // [C] cumulative leapfrog count
+  long long m = 0;            // transitions since the last init_chain_state (:735)
+  long long n_discard = 0;    // warm-up length of the current run (:734)
+};
+
+int nuts_init_state(NutsState* ns, gm_dtype dt, long long C, int D, int max_depth);
+void nuts_free_state(NutsState* ns);
+// progress = 0: NUTS::run semantics; 1: run_progress semantics (see gmcmc.h)
+int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay, void* q,
+             long long* accepts, void* samples, long long C, int D, double target_accept,
+             uint64_t seed, uint64_t* step, uint32_t chain_offset, long long total,
+             long long n_discard, int progress, long long steps_per_launch, hipStream_t st,
+             std::vector<hipEvent_t>& evs, double* ms, long long* launches);
+int nuts_get_step_size(NutsState& ns, gm_dtype dt, long long C, double* eps, double* eps_bar);
+int nuts_get_leapfrogs(NutsState& ns, long long C, long long* out);
+
+}  // namespace gm

@@ -1,0 +1,296 @@
+// gm_rng.h — counter-based randomness and the transcendental functions the
+// samplers need, written so that the host build (g++) and the gfx950 device
+// build (hipcc) produce bit-identical results.
+//
+// Why this exists: the reference draws from rand 0.9 SmallRng + rand_distr
+// (generic_hmc.rs:177,197; generic_nuts.rs:283,767,783,865,1305;
+// metropolis_hastings.rs:313) and from burn's backend-global RNG
+// (euclidean.rs:484-509). Neither stream can be reproduced here (no crate
+// sources), and a serial stream cannot be split across 10^5 chains anyway.
+// Every random number in this engine is instead a pure function
+//     philox4x32_10(counter = {idx, chain, step, tag|step_hi}, key = seed)
+// so a chain's draws do not depend on how chains are placed on lanes, waves or
+// GPUs (bitwise-identical samples at 1/2/4/8 GPUs).
+//
+// Bit-exactness rules (both sides): only IEEE +,-,*,/ and sqrt (correctly
+// rounded on gfx950 and x86), no FMA contraction (-ffp-contract=off), and our
+// own log/exp/cos built from those. The CPU oracle (oracle/gm_oracle.c)
+// restates the same spec independently.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define GM_HD __host__ __device__ __forceinline__
+#else
+#include <math.h>
+#include <string.h>
+#define GM_HD static inline
+#endif
+
+namespace gm {
+
+// Stream tags (counter word 3, low 8 bits).
+enum : uint32_t {
+  TAG_INIT = 1,      // initial positions (core.rs:444-475 init_det analogue)
+  TAG_MOM = 2,       // HMC momentum (batched_hmc.rs:131)
+  TAG_ACC = 3,       // HMC accept uniform (batched_hmc.rs:157)
+  TAG_MH_PROP = 4,   // MH proposal noise (distributions.rs:368-376)
+  TAG_MH_ACC = 5,    // MH accept uniform (metropolis_hastings.rs:313)
+  TAG_NUTS_MOM = 6,  // NUTS momentum (generic_nuts.rs:760)
+  TAG_NUTS_EXP = 7,  // NUTS slice Exp1 (generic_nuts.rs:767)
+  TAG_NUTS_DIR = 8,  // NUTS direction uniform (generic_nuts.rs:783)
+  TAG_NUTS_TOP = 9,  // NUTS top-level accept uniform (generic_nuts.rs:865)
+  TAG_NUTS_MRG = 10, // NUTS subtree-merge f64 uniform (generic_nuts.rs:1305)
+  TAG_NUTS_INIT = 11 // NUTS init momentum for find_reasonable_epsilon (:739)
+};
+
+struct u32x4 { uint32_t x, y, z, w; };
+
+GM_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
+// Philox4x32-10 (Salmon et al., SC'11), the Random123 reference constants.
+GM_HD u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = mulhi32(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = mulhi32(0xCD9E8D57u, c.z);
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+GM_HD u32x4 draw(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  u32x4 c{idx, chain, (uint32_t)step, tag | ((uint32_t)(step >> 32) << 8)};
+  return philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// ---- bit casts -------------------------------------------------------------
+GM_HD uint32_t f2u(float f) {
+#if defined(__HIPCC__)
+  return __builtin_bit_cast(uint32_t, f);
+#else
+  uint32_t u; memcpy(&u, &f, 4); return u;
+#endif
+}
+GM_HD float u2f(uint32_t u) {
+#if defined(__HIPCC__)
+  return __builtin_bit_cast(float, u);
+#else
+  float f; memcpy(&f, &u, 4); return f;
+#endif
+}
+GM_HD uint64_t d2u(double f) {
+#if defined(__HIPCC__)
+  return __builtin_bit_cast(uint64_t, f);
+#else
+  uint64_t u; memcpy(&u, &f, 8); return u;
+#endif
+}
+GM_HD double u2d(uint64_t u) {
+#if defined(__HIPCC__)
+  return __builtin_bit_cast(double, u);
+#else
+  double f; memcpy(&f, &u, 8); return f;
+#endif
+}
+
+GM_HD float gsqrt(float x) {
+#if defined(__HIPCC__)
+  return __builtin_sqrtf(x);
+#else
+  return sqrtf(x);
+#endif
+}
+GM_HD double gsqrt(double x) {
+#if defined(__HIPCC__)
+  return __builtin_sqrt(x);
+#else
+  return sqrt(x);
+#endif
+}
+
+// ---- uniforms ----------------------------------------------------------------
+// [0,1):  f32 = (w>>8)*2^-24 ; f64 = ((a>>5)*2^26 + (b>>6)) * 2^-53
+// (0,1]:  the same integer plus one.
+template <class T> struct Unif;
+template <> struct Unif<float> {
+  GM_HD static float co(uint32_t a, uint32_t) { return (float)(a >> 8) * 5.9604644775390625e-08f; }
+  GM_HD static float oc(uint32_t a, uint32_t) { return (float)((a >> 8) + 1u) * 5.9604644775390625e-08f; }
+};
+template <> struct Unif<double> {
+  GM_HD static double co(uint32_t a, uint32_t b) {
+    const uint64_t k = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+    return (double)k * 1.1102230246251565e-16;
+  }
+  GM_HD static double oc(uint32_t a, uint32_t b) {
+    const uint64_t k = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+    return (double)(k + 1u) * 1.1102230246251565e-16;
+  }
+};
+
+// ---- log (FreeBSD msun e_log.c / e_logf.c polynomials) ----------------------
+GM_HD double glog(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+               Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  uint64_t u = d2u(x);
+  if (x != x) return x;                      // NaN
+  if (x < 0.0) return u2d(0x7ff8000000000000ull);
+  if (x == 0.0) return -u2d(0x7ff0000000000000ull);
+  if ((u >> 52) >= 0x7ff) return x;          // +inf
+  int k = 0;
+  if ((u >> 52) == 0) { x = x * 18014398509481984.0; u = d2u(x); k = -54; }  // subnormal: *2^54
+  k += (int)(u >> 52) - 1023;
+  double m = u2d((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull);  // [1,2)
+  if (m > 1.4142135623730951) { m = m * 0.5; k += 1; }
+  const double f = m - 1.0;
+  const double s = f / (2.0 + f);
+  const double z = s * s, w = z * z;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)k;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+GM_HD float glog(float x) {
+  const float ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f;
+  const float Lg1 = 0.66666662693f, Lg2 = 0.40000972152f, Lg3 = 0.28498786688f, Lg4 = 0.24279078841f;
+  uint32_t u = f2u(x);
+  if (x != x) return x;
+  if (x < 0.0f) return u2f(0x7fc00000u);
+  if (x == 0.0f) return -u2f(0x7f800000u);
+  if ((u >> 23) >= 0xff) return x;
+  int k = 0;
+  if ((u >> 23) == 0) { x = x * 33554432.0f; u = f2u(x); k = -25; }  // subnormal: *2^25
+  k += (int)(u >> 23) - 127;
+  float m = u2f((u & 0x007fffffu) | 0x3f800000u);
+  if (m > 1.41421353816986083984f) { m = m * 0.5f; k += 1; }
+  const float f = m - 1.0f;
+  const float s = f / (2.0f + f);
+  const float z = s * s, w = z * z;
+  const float t1 = w * (Lg2 + w * Lg4);
+  const float t2 = z * (Lg1 + w * Lg3);
+  const float R = t2 + t1;
+  const float hfsq = 0.5f * f * f;
+  const float dk = (float)k;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+// ---- exp (FreeBSD msun e_exp.c / e_expf.c) -----------------------------------
+GM_HD double scale2(double y, int k) {  // y * 2^k, y in [0.5, 2]
+  if (k > 1023) return y * u2d(0x7fe0000000000000ull) * u2d((uint64_t)(k - 1023 + 1023) << 52);
+  if (k < -1021) return y * u2d((uint64_t)(k + 1000 + 1023) << 52) * u2d((uint64_t)(-1000 + 1023) << 52);
+  return y * u2d((uint64_t)(k + 1023) << 52);
+}
+GM_HD double gexp(double x) {
+  const double o_th = 7.09782712893383973096e+02, u_th = -7.45133219101941108420e+02;
+  const double ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10;
+  const double invln2 = 1.44269504088896338700e+00;
+  const double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+               P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+               P5 = 4.13813679705723846039e-08;
+  if (x != x) return x;
+  if (x > o_th) return u2d(0x7ff0000000000000ull);
+  if (x < u_th) return 0.0;
+  const int k = (int)(invln2 * x + (x < 0.0 ? -0.5 : 0.5));
+  const double dk = (double)k;
+  const double hi = x - dk * ln2HI, lo = dk * ln2LO;
+  const double r = hi - lo;
+  const double t = r * r;
+  const double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+  const double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
+  return scale2(y, k);
+}
+GM_HD float scale2f(float y, int k) {
+  if (k > 127) return y * u2f(0x7f000000u) * u2f((uint32_t)(k - 127 + 127) << 23);
+  if (k < -125) return y * u2f((uint32_t)(k + 100 + 127) << 23) * u2f((uint32_t)(-100 + 127) << 23);
+  return y * u2f((uint32_t)(k + 127) << 23);
+}
+GM_HD float gexp(float x) {
+  const float o_th = 8.8721679688e+01f, u_th = -1.0397208405e+02f;
+  const float ln2HI = 6.9314575195e-01f, ln2LO = 1.4286067653e-06f, invln2 = 1.4426950216e+00f;
+  const float P1 = 1.6666625440e-1f, P2 = -2.7667332906e-3f;
+  if (x != x) return x;
+  if (x > o_th) return u2f(0x7f800000u);
+  if (x < u_th) return 0.0f;
+  const int k = (int)(invln2 * x + (x < 0.0f ? -0.5f : 0.5f));
+  const float dk = (float)k;
+  const float hi = x - dk * ln2HI, lo = dk * ln2LO;
+  const float r = hi - lo;
+  const float t = r * r;
+  const float c = r - t * (P1 + t * P2);
+  const float y = 1.0f - ((lo - (r * c) / (2.0f - c)) - hi);
+  return scale2f(y, k);
+}
+
+// ---- cos(2*pi*u), u in [0,1) -------------------------------------------------
+GM_HD double ksin(double x) {
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  const double z = x * x, v = z * x;
+  const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+  return x + v * (S1 + z * r);
+}
+GM_HD double kcos(double x) {
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  const double z = x * x, w = z * z;
+  const double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+  const double hz = 0.5 * z;
+  const double ww = 1.0 - hz;
+  return ww + (((1.0 - ww) - hz) + z * r);
+}
+GM_HD float ksin(float x) {
+  const float z = x * x;
+  return x + x * z * (-1.6666667163e-01f + z * (8.3333337680e-03f + z * (-1.9841270114e-04f + z * 2.7557314297e-06f)));
+}
+GM_HD float kcos(float x) {
+  const float z = x * x;
+  return 1.0f - 0.5f * z + z * z * (4.1666667908e-02f + z * (-1.3888889225e-03f + z * (2.4801587642e-05f + z * -2.7557314297e-07f)));
+}
+template <class T> GM_HD T cos2pi(T u) {
+  const T twopi = (T)6.283185307179586476925286766559;
+  T a = u;                          // u in [0,1)
+  if (a > (T)0.5) a = (T)1.0 - a;   // cos(2pi u) = cos(2pi (1-u)); 1-u exact for u in (0.5,1)
+  T sign = (T)1.0;
+  if (a > (T)0.25) { a = (T)0.5 - a; sign = (T)-1.0; }  // cos(pi - x) = -cos x
+  T r;
+  if (a <= (T)0.125) r = kcos(a * twopi);
+  else r = ksin(((T)0.25 - a) * twopi);               // cos(pi/2 - y) = sin y
+  return sign * r;
+}
+
+// ---- standard normal (Box-Muller, cosine branch) and Exp1 ------------------
+template <class T> GM_HD T normal_from(u32x4 x) {
+  const T u1 = Unif<T>::oc(x.x, x.y);          // (0,1]
+  const T u2 = Unif<T>::co(x.z, x.w);          // [0,1)
+  const T r = gsqrt((T)-2.0 * glog(u1));
+  return r * cos2pi<T>(u2);
+}
+template <class T> GM_HD T normal(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  return normal_from<T>(draw(seed, chain, step, tag, idx));
+}
+template <class T> GM_HD T uniform_co(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  const u32x4 x = draw(seed, chain, step, tag, idx);
+  return Unif<T>::co(x.x, x.y);
+}
+template <class T> GM_HD T uniform_oc(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  const u32x4 x = draw(seed, chain, step, tag, idx);
+  return Unif<T>::oc(x.x, x.y);
+}
+template <class T> GM_HD T exp1(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  return -glog(uniform_oc<T>(seed, chain, step, tag, idx));
+}
+
+}  // namespace gm

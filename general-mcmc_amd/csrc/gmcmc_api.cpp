@@ -1,0 +1,660 @@
+// gmcmc_api.cpp — the C ABI (include/gmcmc.h): sampler objects, device
+// memory, streams, run orchestration and error reporting.
+//
+// Orchestration mirrors the reference facades:
+//   HMC::new / run / run_positions      hmc.rs:113-181, batched_hmc.rs:62-123
+//   MetropolisHastings + ChainRunner    metropolis_hastings.rs:151-197, core.rs:95-115,219-229
+//   NUTS::new / run / run_progress      nuts.rs:156-304, generic_nuts.rs:592-753
+// but a transition of all chains is one fused kernel step, and many steps run
+// inside one launch with the chain state resident in registers.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "gm_layouts.h"
+#include "gm_nuts.h"
+#include "gm_rng.h"
+
+namespace gm {
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+bool layout_supported(int lanes, int elems) {
+#define GM_CHECK_LAYOUT(L_, E_) \
+  if (lanes == L_ && elems == E_) return true;
+  GM_LAYOUT_LIST(GM_CHECK_LAYOUT)
+#undef GM_CHECK_LAYOUT
+  return false;
+}
+
+static int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+Layout default_layout(int D, gm_dtype dt, int kind) {
+  (void)dt;
+  (void)kind;
+  Layout l;
+  if (D <= 64) {
+    l.elems = 1;
+    l.lanes = next_pow2(D < 1 ? 1 : D);
+  } else if (D <= 128) {
+    l.lanes = 64;
+    l.elems = 2;
+  } else if (D <= 256) {
+    l.lanes = 64;
+    l.elems = 4;
+  } else if (D <= 512) {
+    l.lanes = 64;
+    l.elems = 8;
+  } else {
+    l.lanes = 64;
+    l.elems = 16;
+  }
+  return l;
+}
+}  // namespace gm
+
+using namespace gm;
+
+#define GM_HIP(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess) {                                                            \
+      set_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " #expr);     \
+      return GM_EHIP;                                                                  \
+    }                                                                                  \
+  } while (0)
+
+#define GM_REQ(cond, msg)      \
+  do {                         \
+    if (!(cond)) {             \
+      set_error(msg);          \
+      return GM_EINVAL;        \
+    }                          \
+  } while (0)
+
+enum SamplerKind { K_HMC = 1, K_MH = 2, K_NUTS = 3 };
+
+struct gm_sampler {
+  int kind = 0;
+  gm_dtype dt = GM_F32;
+  size_t esz = 4;
+  long long C = 0;
+  int D = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  TargetDev tg;
+  void* d_mu = nullptr;
+  void* d_prec = nullptr;
+  double eps = 0;
+  int L = 0;
+  double prop_std = 1;
+  double target_accept = 0.8;
+  int max_depth = 10;
+  uint64_t seed = 0;
+  uint64_t step = 0;
+  uint32_t chain_offset = 0;
+  void* d_q = nullptr;
+  void* d_logp = nullptr;
+  long long* d_acc = nullptr;
+  void* d_samples = nullptr;
+  size_t samples_bytes = 0;
+  void* d_tmp = nullptr;
+  size_t tmp_bytes = 0;
+  Layout lay;
+  long long steps_per_launch = 1000;
+  std::vector<hipEvent_t> evs;
+  double last_ms = 0;
+  long long last_launches = 0;
+  long long total_steps = 0;  // transitions since creation
+  long long last_rows = 0;    // sample rows produced by the last run
+  NutsState nuts;
+};
+
+static int ensure_buf(void** p, size_t* cap, size_t need) {
+  if (*cap >= need) return GM_OK;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  if (need == 0) return GM_OK;
+  hipError_t e = hipMalloc(p, need);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    set_error(std::string("device allocation of ") + std::to_string(need) + " bytes failed: " +
+              hipGetErrorString(e));
+    return GM_ENOMEM;
+  }
+  *cap = need;
+  return GM_OK;
+}
+
+// Copy a double array to device as dtype.
+static int upload_as(gm_dtype dt, const double* src, size_t n, void** dst) {
+  const size_t esz = dt == GM_F32 ? 4 : 8;
+  std::vector<unsigned char> tmp(n * esz);
+  for (size_t i = 0; i < n; ++i) {
+    if (dt == GM_F32) {
+      float v = (float)src[i];
+      memcpy(&tmp[i * 4], &v, 4);
+    } else {
+      memcpy(&tmp[i * 8], &src[i], 8);
+    }
+  }
+  GM_HIP(hipMalloc(dst, n * esz));
+  GM_HIP(hipMemcpy(*dst, tmp.data(), n * esz, hipMemcpyHostToDevice));
+  return GM_OK;
+}
+
+static int build_target(const gm_target* t, gm_dtype dt, long long dim, TargetDev* out, void** d_mu,
+                        void** d_prec) {
+  GM_REQ(t != nullptr, "target is NULL");
+  GM_REQ(t->dim == dim, "target dim does not match the sampler dim");
+  GM_REQ(dim >= 1 && dim <= 1024, "dim must be in [1, 1024]");
+  out->kind = t->kind;
+  out->D = (int)dim;
+  out->a = t->a;
+  out->b = t->b;
+  out->std = t->std;
+  out->norm_const = t->norm_const;
+  switch (t->kind) {
+    case GM_TARGET_ROSENBROCK:
+      break;
+    case GM_TARGET_ISO_GAUSS:
+      GM_REQ(t->std > 0, "ISO_GAUSS std must be > 0");
+      break;
+    case GM_TARGET_GAUSS: {
+      GM_REQ(t->mean != nullptr && t->prec != nullptr, "GAUSS needs mean and prec");
+      int rc = upload_as(dt, t->mean, (size_t)dim, d_mu);
+      if (rc) return rc;
+      rc = upload_as(dt, t->prec, (size_t)(dim * dim), d_prec);
+      if (rc) return rc;
+      out->mu = *d_mu;
+      out->prec = *d_prec;
+      break;
+    }
+    default:
+      GM_REQ(false, "unknown target kind");
+  }
+  return GM_OK;
+}
+
+extern "C" {
+
+const char* gm_last_error(void) { return g_err.c_str(); }
+
+int gm_device_count(int* count) {
+  GM_REQ(count, "count is NULL");
+  GM_HIP(hipGetDeviceCount(count));
+  return GM_OK;
+}
+
+int gm_set_device(int device) {
+  GM_HIP(hipSetDevice(device));
+  return GM_OK;
+}
+
+int gm_device_synchronize(void) {
+  GM_HIP(hipDeviceSynchronize());
+  return GM_OK;
+}
+
+// DiffableGaussian2D::new (distributions.rs:229-253); dim > 2 via the
+// reference's own Cholesky / inverse (generic_nuts.rs:306-359).
+int gm_gauss_from_cov(int64_t dim, const double* cov, double* prec, double* nc) {
+  GM_REQ(dim >= 1 && cov && prec && nc, "bad arguments");
+  const double pi = 3.14159265358979323846;
+  if (dim == 2) {
+    const double det = cov[0] * cov[3] - cov[1] * cov[2];
+    GM_REQ(det > 0, "covariance is not positive definite");
+    const double inv_det = 1.0 / det;
+    prec[0] = cov[3] * inv_det;
+    prec[1] = -cov[1] * inv_det;
+    prec[2] = -cov[2] * inv_det;
+    prec[3] = cov[0] * inv_det;
+    const double logdet = std::log(det);
+    const double two = 1.0 + 1.0;
+    *nc = -(two * std::log(two * pi) + logdet) / two;
+    return GM_OK;
+  }
+  const long long n = dim;
+  std::vector<double> l(n * n, 0.0), inv_l(n * n, 0.0);
+  for (long long i = 0; i < n; ++i)
+    for (long long j = 0; j <= i; ++j) {
+      double sum = cov[i * n + j];
+      for (long long k = 0; k < j; ++k) sum -= l[i * n + k] * l[j * n + k];
+      if (i == j) {
+        GM_REQ(sum > 0 && std::isfinite(sum), "covariance is not positive definite");
+        l[i * n + j] = std::sqrt(sum);
+      } else {
+        l[i * n + j] = sum / l[j * n + j];
+      }
+    }
+  double logdet = 0;
+  for (long long i = 0; i < n; ++i) logdet += 2.0 * std::log(l[i * n + i]);
+  for (long long i = 0; i < n; ++i) {
+    inv_l[i * n + i] = 1.0 / l[i * n + i];
+    for (long long j = i + 1; j < n; ++j) {
+      double sum = 0;
+      for (long long k = i; k < j; ++k) sum += l[j * n + k] * inv_l[k * n + i];
+      inv_l[j * n + i] = -sum / l[j * n + j];
+    }
+  }
+  for (long long i = 0; i < n; ++i)
+    for (long long j = 0; j <= i; ++j) {
+      double sum = 0;
+      for (long long k = (i > j ? i : j); k < n; ++k) sum += inv_l[k * n + i] * inv_l[k * n + j];
+      prec[i * n + j] = sum;
+      prec[j * n + i] = sum;
+    }
+  *nc = -((double)n * std::log(2.0 * pi) + logdet) / 2.0;
+  return GM_OK;
+}
+
+int gm_init_positions(uint64_t seed, int64_t n, int64_t dim, gm_dtype dtype, void* out) {
+  GM_REQ(n >= 0 && dim >= 0 && (out || n * dim == 0), "bad arguments");
+  GM_REQ(dtype == GM_F32 || dtype == GM_F64, "bad dtype");
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t d = 0; d < dim; ++d) {
+      const double z = normal<double>(seed, (uint32_t)i, 0, TAG_INIT, (uint32_t)d);
+      if (dtype == GM_F32) ((float*)out)[i * dim + d] = (float)z;
+      else ((double*)out)[i * dim + d] = z;
+    }
+  return GM_OK;
+}
+
+int gm_target_logp_grad(const gm_target* target, gm_dtype dtype, int64_t n, const void* x,
+                        void* logp_out, void* grad_out) {
+  GM_REQ(dtype == GM_F32 || dtype == GM_F64, "bad dtype");
+  GM_REQ(n >= 0 && (n == 0 || x), "bad arguments");
+  GM_REQ(target != nullptr, "target is NULL");
+  TargetDev tg;
+  void *d_mu = nullptr, *d_prec = nullptr;
+  int rc = build_target(target, dtype, target->dim, &tg, &d_mu, &d_prec);
+  if (rc) return rc;
+  const size_t esz = dtype == GM_F32 ? 4 : 8;
+  const long long D = target->dim;
+  void *dx = nullptr, *dl = nullptr, *dg = nullptr;
+  int out = GM_OK;
+  if (n > 0) {
+    if (hipMalloc(&dx, n * D * esz) != hipSuccess || hipMalloc(&dl, n * esz) != hipSuccess ||
+        hipMalloc(&dg, n * D * esz) != hipSuccess) {
+      set_error("device allocation failed");
+      out = GM_ENOMEM;
+    } else {
+      hipMemcpy(dx, x, n * D * esz, hipMemcpyHostToDevice);
+      Layout lay = default_layout((int)D, dtype, target->kind);
+      hipError_t e = launch_logp_grad(dtype, tg, lay, n, dx, dl, dg, nullptr);
+      if (e == hipSuccess) e = hipDeviceSynchronize();
+      if (e != hipSuccess) {
+        set_error(std::string("logp_grad launch failed: ") + hipGetErrorString(e));
+        out = GM_EHIP;
+      } else {
+        if (logp_out) hipMemcpy(logp_out, dl, n * esz, hipMemcpyDeviceToHost);
+        if (grad_out) hipMemcpy(grad_out, dg, n * D * esz, hipMemcpyDeviceToHost);
+      }
+    }
+  }
+  if (dx) hipFree(dx);
+  if (dl) hipFree(dl);
+  if (dg) hipFree(dg);
+  if (d_mu) hipFree(d_mu);
+  if (d_prec) hipFree(d_prec);
+  return out;
+}
+
+static int create_common(int kind, const gm_target* target, gm_dtype dtype, int64_t n_chains,
+                         int64_t dim, const void* init, int64_t chain_offset, gm_sampler** out) {
+  GM_REQ(out != nullptr, "out is NULL");
+  *out = nullptr;
+  GM_REQ(dtype == GM_F32 || dtype == GM_F64, "bad dtype");
+  GM_REQ(n_chains >= 1, "n_chains must be >= 1");
+  GM_REQ(init != nullptr, "init is NULL");
+  GM_REQ(chain_offset >= 0 && chain_offset + n_chains <= 0xffffffffLL,
+         "global chain ids must fit in 32 bits");
+  gm_sampler* s = new gm_sampler();
+  s->kind = kind;
+  s->dt = dtype;
+  s->esz = dtype == GM_F32 ? 4 : 8;
+  s->C = n_chains;
+  s->D = (int)dim;
+  s->chain_offset = (uint32_t)chain_offset;
+  std::random_device rd;
+  s->seed = ((uint64_t)rd() << 32) ^ rd();  // reference: SmallRng::from_rng(thread rng)
+  int rc = build_target(target, dtype, dim, &s->tg, &s->d_mu, &s->d_prec);
+  if (rc) {
+    gm_destroy(s);
+    return rc;
+  }
+  s->lay = default_layout((int)dim, dtype, target->kind);
+  hipError_t e = hipGetDevice(&s->device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&s->d_q, n_chains * dim * s->esz);
+  if (e == hipSuccess) e = hipMalloc(&s->d_logp, n_chains * s->esz);
+  if (e == hipSuccess) e = hipMalloc((void**)&s->d_acc, n_chains * sizeof(long long));
+  if (e == hipSuccess) e = hipMemcpy(s->d_q, init, n_chains * dim * s->esz, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(s->d_acc, 0, n_chains * sizeof(long long));
+  if (e != hipSuccess) {
+    set_error(std::string("sampler setup failed: ") + hipGetErrorString(e));
+    gm_destroy(s);
+    return GM_EHIP;
+  }
+  *out = s;
+  return GM_OK;
+}
+
+int gm_hmc_create(const gm_target* target, gm_dtype dtype, int64_t n_chains, int64_t dim,
+                  const void* init, double step_size, int64_t n_leapfrog, int64_t chain_offset,
+                  gm_sampler** out) {
+  GM_REQ(n_leapfrog >= 0 && n_leapfrog < (1 << 30), "n_leapfrog out of range");
+  GM_REQ(std::isfinite(step_size), "step_size must be finite");
+  int rc = create_common(K_HMC, target, dtype, n_chains, dim, init, chain_offset, out);
+  if (rc) return rc;
+  (*out)->eps = step_size;
+  (*out)->L = (int)n_leapfrog;
+  return GM_OK;
+}
+
+int gm_mh_create(const gm_target* target, gm_dtype dtype, int64_t n_chains, int64_t dim,
+                 const void* init, double proposal_std, int64_t chain_offset, gm_sampler** out) {
+  GM_REQ(proposal_std > 0 && std::isfinite(proposal_std), "proposal_std must be > 0");
+  int rc = create_common(K_MH, target, dtype, n_chains, dim, init, chain_offset, out);
+  if (rc) return rc;
+  (*out)->prop_std = proposal_std;
+  return GM_OK;
+}
+
+int gm_nuts_create(const gm_target* target, gm_dtype dtype, int64_t n_chains, int64_t dim,
+                   const void* init, double target_accept_p, int32_t max_depth,
+                   int64_t chain_offset, gm_sampler** out) {
+  GM_REQ(max_depth >= 0 && max_depth <= NUTS_MAX_DEPTH_LIMIT, "max_depth out of range");
+  int rc = create_common(K_NUTS, target, dtype, n_chains, dim, init, chain_offset, out);
+  if (rc) return rc;
+  gm_sampler* s = *out;
+  s->target_accept = target_accept_p;
+  s->max_depth = max_depth == 0 ? NUTS_DEFAULT_MAX_DEPTH : max_depth;
+  rc = nuts_init_state(&s->nuts, s->dt, s->C, s->D, s->max_depth);
+  if (rc) {
+    gm_destroy(s);
+    *out = nullptr;
+    return rc;
+  }
+  return GM_OK;
+}
+
+int gm_set_seed(gm_sampler* s, uint64_t seed) {
+  GM_REQ(s, "sampler is NULL");
+  s->seed = seed;
+  s->step = 0;
+  return GM_OK;
+}
+
+int gm_sampler_layout(gm_sampler* s, int32_t* lanes, int32_t* elems) {
+  GM_REQ(s, "sampler is NULL");
+  if (lanes) *lanes = s->lay.lanes;
+  if (elems) *elems = s->lay.elems;
+  return GM_OK;
+}
+
+int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(layout_supported(lanes, elems), "layout (lanes, elems) is not compiled in");
+  GM_REQ((long long)lanes * elems >= s->D, "lanes*elems must cover dim");
+  GM_REQ((long long)lanes * elems < 2LL * s->D || lanes == 1 ||
+             ((long long)(lanes / 2) * elems < s->D),
+         "layout wastes more than half of its lanes");
+  s->lay.lanes = lanes;
+  s->lay.elems = elems;
+  return GM_OK;
+}
+
+int gm_sampler_set_steps_per_launch(gm_sampler* s, int64_t steps) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(steps >= 1, "steps must be >= 1");
+  s->steps_per_launch = steps;
+  return GM_OK;
+}
+
+int gm_sampler_last_run_stats(gm_sampler* s, double* kernel_ms, int64_t* launches) {
+  GM_REQ(s, "sampler is NULL");
+  if (kernel_ms) *kernel_ms = s->last_ms;
+  if (launches) *launches = s->last_launches;
+  return GM_OK;
+}
+
+// Runs `total` transitions; transitions with index >= collect_from (0-based
+// within this call) are stored at sample rows (index - collect_from).
+static int run_steps(gm_sampler* s, long long total, long long collect_from, int progress) {
+  GM_HIP(hipSetDevice(s->device));
+  s->last_ms = 0;
+  s->last_launches = 0;
+  if (total <= 0) return GM_OK;
+  if (s->kind == K_NUTS) {
+    int rc = nuts_run(s->nuts, s->dt, s->tg, s->lay, s->d_q, s->d_acc, s->d_samples, s->C, s->D,
+                      s->target_accept, s->seed, &s->step, s->chain_offset, total, collect_from,
+                      progress, s->steps_per_launch, s->stream, s->evs, &s->last_ms,
+                      &s->last_launches);
+    return rc;
+  }
+  const long long chunk = s->steps_per_launch;
+  const long long n_launch = (total + chunk - 1) / chunk;
+  while ((long long)s->evs.size() < 2 * n_launch) {
+    hipEvent_t ev;
+    GM_HIP(hipEventCreate(&ev));
+    s->evs.push_back(ev);
+  }
+  long long li = 0;
+  for (long long start = 0; start < total; start += chunk, ++li) {
+    const long long n = total - start < chunk ? total - start : chunk;
+    long long cf = collect_from - start;
+    if (cf < 0) cf = 0;
+    if (cf > n) cf = n;
+    long long row0 = start - collect_from;
+    if (row0 < 0) row0 = 0;
+    GM_HIP(hipEventRecord(s->evs[2 * li], s->stream));
+    hipError_t e;
+    if (s->kind == K_HMC) {
+      HmcLaunch a;
+      a.q = s->d_q;
+      a.logp = s->d_logp;
+      a.accepts = s->d_acc;
+      a.samples = s->d_samples;
+      a.C = s->C;
+      a.D = s->D;
+      a.eps = s->eps;
+      a.L = s->L;
+      a.seed = s->seed;
+      a.step0 = s->step + start;
+      a.chain_offset = s->chain_offset;
+      a.n_steps = (int)n;
+      a.collect_from = (int)cf;
+      a.sample_row0 = row0;
+      e = launch_hmc(s->dt, s->tg, s->lay, a, s->stream);
+    } else {
+      MhLaunch a;
+      a.q = s->d_q;
+      a.logp = s->d_logp;
+      a.accepts = s->d_acc;
+      a.samples = s->d_samples;
+      a.C = s->C;
+      a.D = s->D;
+      a.prop_std = s->prop_std;
+      a.seed = s->seed;
+      a.step0 = s->step + start;
+      a.chain_offset = s->chain_offset;
+      a.n_steps = (int)n;
+      a.collect_from = (int)cf;
+      a.sample_row0 = row0;
+      e = launch_mh(s->dt, s->tg, s->lay, a, s->stream);
+    }
+    if (e != hipSuccess) {
+      set_error(std::string("kernel launch failed: ") + hipGetErrorString(e));
+      return GM_EHIP;
+    }
+    GM_HIP(hipEventRecord(s->evs[2 * li + 1], s->stream));
+  }
+  s->step += total;
+  s->total_steps += total;
+  GM_HIP(hipStreamSynchronize(s->stream));
+  double ms = 0;
+  for (long long i = 0; i < n_launch; ++i) {
+    float t = 0;
+    GM_HIP(hipEventElapsedTime(&t, s->evs[2 * i], s->evs[2 * i + 1]));
+    ms += t;
+  }
+  s->last_ms = ms;
+  s->last_launches = n_launch;
+  return GM_OK;
+}
+
+static int run_impl(gm_sampler* s, int64_t n_collect, int64_t n_discard, int progress) {
+  GM_REQ(s, "sampler is NULL");
+  s->last_rows = n_collect;
+  GM_REQ(n_collect >= 0 && n_discard >= 0, "n_collect and n_discard must be >= 0");
+  GM_HIP(hipSetDevice(s->device));
+  int rc = ensure_buf(&s->d_samples, &s->samples_bytes, (size_t)n_collect * s->C * s->D * s->esz);
+  if (rc) return rc;
+  long long total = n_discard + n_collect;
+  if (s->kind == K_NUTS && !progress) {
+    // NUTS::run performs n_collect + n_discard - 1 transitions (nuts.rs:232-257);
+    // row r is the state after n_discard + r of them.
+    if (n_collect == 0) return GM_OK;
+    total = n_discard + n_collect - 1;
+    return run_steps(s, total, n_discard, progress ? 1 : 0);
+  }
+  return run_steps(s, total, n_discard, progress ? 1 : 0);
+}
+
+int gm_run_device(gm_sampler* s, int64_t n_collect, int64_t n_discard, const void** dev_samples) {
+  int rc = run_impl(s, n_collect, n_discard, 0);
+  if (rc) return rc;
+  if (dev_samples) *dev_samples = s->d_samples;
+  return GM_OK;
+}
+
+int gm_run_device_progress(gm_sampler* s, int64_t n_collect, int64_t n_discard,
+                           const void** dev_samples) {
+  int rc = run_impl(s, n_collect, n_discard, 1);
+  if (rc) return rc;
+  if (dev_samples) *dev_samples = s->d_samples;
+  return GM_OK;
+}
+
+int gm_copy_samples(gm_sampler* s, void* out) {
+  GM_REQ(s && out, "bad arguments");
+  GM_HIP(hipSetDevice(s->device));
+  const long long n_collect = s->last_rows;
+  if (n_collect == 0) return GM_OK;
+  const size_t bytes = (size_t)n_collect * s->C * s->D * s->esz;
+  int rc = ensure_buf(&s->d_tmp, &s->tmp_bytes, bytes);
+  if (rc) return rc;
+  hipError_t e = launch_transpose_samples(s->dt, s->d_samples, s->d_tmp, n_collect, s->C, s->D,
+                                          s->stream);
+  if (e != hipSuccess) {
+    set_error(std::string("transpose failed: ") + hipGetErrorString(e));
+    return GM_EHIP;
+  }
+  GM_HIP(hipMemcpyAsync(out, s->d_tmp, bytes, hipMemcpyDeviceToHost, s->stream));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  return GM_OK;
+}
+
+int gm_run(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out) {
+  int rc = run_impl(s, n_collect, n_discard, 0);
+  if (rc) return rc;
+  if (!out || n_collect == 0) return GM_OK;
+  return gm_copy_samples(s, out);
+}
+
+int gm_run_progress(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out,
+                    float* rhat_out, float* ess_out) {
+  int rc = run_impl(s, n_collect, n_discard, 1);
+  if (rc) return rc;
+  if (out && n_collect > 0) {
+    rc = gm_copy_samples(s, out);
+    if (rc) return rc;
+  }
+  if (rhat_out || ess_out) {
+    GM_REQ(n_collect >= 2, "run_progress statistics need n_collect >= 2");
+    std::vector<float> r(s->D), e(s->D);
+    rc = gm_split_rhat_ess_device(s->d_samples, s->dt, s->C, n_collect, s->D, s->D,
+                                  s->C * s->D, 1, r.data(), e.data());
+    if (rc) return rc;
+    if (rhat_out) memcpy(rhat_out, r.data(), sizeof(float) * s->D);
+    if (ess_out) memcpy(ess_out, e.data(), sizeof(float) * s->D);
+  }
+  return GM_OK;
+}
+
+int gm_step(gm_sampler* s) {
+  GM_REQ(s, "sampler is NULL");
+  return run_steps(s, 1, 1, 0);
+}
+
+int gm_get_positions(gm_sampler* s, void* out) {
+  GM_REQ(s && out, "bad arguments");
+  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  GM_HIP(hipMemcpy(out, s->d_q, s->C * s->D * s->esz, hipMemcpyDeviceToHost));
+  return GM_OK;
+}
+
+int gm_set_positions(gm_sampler* s, const void* in) {
+  GM_REQ(s && in, "bad arguments");
+  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  GM_HIP(hipMemcpy(s->d_q, in, s->C * s->D * s->esz, hipMemcpyHostToDevice));
+  return GM_OK;
+}
+
+int gm_get_accept_counts(gm_sampler* s, int64_t* out) {
+  GM_REQ(s && out, "bad arguments");
+  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  GM_HIP(hipMemcpy(out, s->d_acc, s->C * sizeof(long long), hipMemcpyDeviceToHost));
+  return GM_OK;
+}
+
+int gm_get_leapfrog_counts(gm_sampler* s, int64_t* out) {
+  GM_REQ(s && out, "bad arguments");
+  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  if (s->kind == K_NUTS) return nuts_get_leapfrogs(s->nuts, s->C, (long long*)out);
+  for (long long i = 0; i < s->C; ++i) out[i] = s->kind == K_HMC ? (int64_t)s->total_steps * s->L : 0;
+  return GM_OK;
+}
+
+int gm_nuts_get_step_size(gm_sampler* s, double* eps, double* eps_bar) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");
+  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  return nuts_get_step_size(s->nuts, s->dt, s->C, eps, eps_bar);
+}
+
+int gm_destroy(gm_sampler* s) {
+  if (!s) return GM_OK;
+  hipSetDevice(s->device);
+  if (s->stream) hipStreamSynchronize(s->stream);
+  for (auto ev : s->evs) hipEventDestroy(ev);
+  if (s->d_mu) hipFree(s->d_mu);
+  if (s->d_prec) hipFree(s->d_prec);
+  if (s->d_q) hipFree(s->d_q);
+  if (s->d_logp) hipFree(s->d_logp);
+  if (s->d_acc) hipFree(s->d_acc);
+  if (s->d_samples) hipFree(s->d_samples);
+  if (s->d_tmp) hipFree(s->d_tmp);
+  nuts_free_state(&s->nuts);
+  if (s->stream) hipStreamDestroy(s->stream);
+  delete s;
+  return GM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,126 @@
+// hmc_kernels.hip — fused many-chain HMC transition kernel for gfx950.
+//
+// Replaces BatchedGenericHMC::step + leapfrog (batched_hmc.rs:129-190) and the
+// BatchVector ops it calls on Tensor<B,2> (euclidean.rs:447-534): momentum
+// draw (484-496), kinetic energy (464-472), add_scaled_assign kick/drift
+// (392-394), log-density+gradient (hmc.rs:42-61), accept mask (527-533) and
+// masked_assign (474-482).
+//
+// One launch runs `n_steps` full transitions for every chain; a chain's
+// position, momentum and gradient live in VGPRs for the whole launch, so HBM
+// sees one read and one write of the state per launch plus the collected
+// samples. Arithmetic follows the reference's operation order with no FMA
+// contraction (built with -ffp-contract=off):
+//   p <- p + g*(0.5*eps);  q <- q + p*eps;  (logp, g) <- target(q);  p <- p + g*(0.5*eps)
+//   K = (sum p*p) * 0.5;  log_alpha = (logp' - logp) + (K - K');  accept iff log_alpha >= ln u
+// The gradient at the current point is carried across transitions (the
+// reference re-evaluates it twice per step, batched_hmc.rs:138,169; same
+// values), so a transition costs exactly L target evaluations.
+#include "gm_layouts.h"
+
+namespace gm {
+
+template <class T, int LPC, int E, class TG>
+__global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg) {
+  const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long c = gtid / LPC;
+  const int lane = (int)(gtid % LPC);
+  if (c >= a.C) return;  // whole lane groups leave together
+  const int D = a.D;
+  T* __restrict__ qs = (T*)a.q;
+  const T eps = (T)a.eps;
+  const T half = (T)0.5 * eps;  // batched_hmc.rs:167
+  const uint32_t cid = a.chain_offset + (uint32_t)c;
+
+  T q[E], g[E], p[E], q1[E], p1[E], g1[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    q[e] = (i < D) ? qs[c * D + i] : (T)0;
+  }
+  T lp = tg.template eval<LPC, E, true>(q, g, lane);
+  long long acc = 0;
+
+  for (int s = 0; s < a.n_steps; ++s) {
+    const uint64_t st = a.step0 + (uint64_t)s;
+    // 1. momentum ~ N(0, I)
+    T kp = (T)0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      p[e] = (i < D) ? normal<T>(a.seed, cid, st, TAG_MOM, (uint32_t)i) : (T)0;
+      const T sq = p[e] * p[e];
+      kp = (e == 0) ? sq : kp + sq;
+    }
+    // 2. kinetic energy
+    const T ke0 = group_sum<LPC>(kp) * (T)0.5;
+    // 4. proposal buffers
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      q1[e] = q[e];
+      p1[e] = p[e];
+      g1[e] = g[e];
+    }
+    // 5. leapfrog
+    T lp1 = lp;
+    for (int l = 0; l < a.L; ++l) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+#pragma unroll
+      for (int e = 0; e < E; ++e) q1[e] = q1[e] + p1[e] * eps;
+      if (l + 1 < a.L) tg.template eval<LPC, E, false>(q1, g1, lane);
+      else lp1 = tg.template eval<LPC, E, true>(q1, g1, lane);
+#pragma unroll
+      for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+    }
+    // 6. proposed kinetic energy
+    T kq = (T)0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const T sq = p1[e] * p1[e];
+      kq = (e == 0) ? sq : kq + sq;
+    }
+    const T ke1 = group_sum<LPC>(kq) * (T)0.5;
+    // 7-9. Metropolis accept (NaN log_alpha rejects)
+    const T log_alpha = (lp1 - lp) + (ke0 - ke1);
+    const T lnu = glog(uniform_co<T>(a.seed, cid, st, TAG_ACC, 0u));
+    if (log_alpha >= lnu) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        q[e] = q1[e];
+        g[e] = g1[e];
+      }
+      lp = lp1;
+      ++acc;
+    }
+    if (s >= a.collect_from) {
+      T* __restrict__ out = (T*)a.samples + ((a.sample_row0 + (s - a.collect_from)) * a.C + c) * D;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        if (i < D) out[i] = q[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    if (i < D) qs[c * D + i] = q[e];
+  }
+  if (lane == 0) {
+    ((T*)a.logp)[c] = lp;
+    a.accepts[c] += acc;
+  }
+}
+
+hipError_t launch_hmc(gm_dtype dt, const TargetDev& tg, const Layout& lay, const HmcLaunch& a,
+                      hipStream_t st) {
+  return dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
+    const long long threads = a.C * LPC;
+    const unsigned blocks = (unsigned)((threads + 255) / 256);
+    hipLaunchKernelGGL((hmc_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), 0, st, a, t);
+    return hipGetLastError();
+  });
+}
+
+}  // namespace gm

@@ -1,0 +1,555 @@
+// nuts_kernels.hip — many-chain No-U-Turn sampler for gfx950.
+//
+// Restates GenericNUTSChain::step (generic_nuts.rs:755-925) with the identity
+// mass matrix that NUTS::new selects (generic_nuts.rs:370-377), including the
+// reference's variant details:
+//   * slice variable logu = joint - Exp1                         (:765-768)
+//   * leaf: n' = [logu < joint], s' = [logu - 1000 < joint],
+//           alpha' = min(1, exp(joint - joint0)) (Rust min: NaN -> 1) (:1197-1207)
+//   * merge: right-half proposal taken iff U_f64 < n''/max(n'+n'',1)  (:1305-1306)
+//           s' &= s'' & U-turn(endpoints, identity mass)            (:1316-1323)
+//   * top level: move iff s' & U < min(1, n'/n), n starts at 1       (:860-868)
+//   * dual averaging from the LAST subtree's alpha/n_alpha only      (:882-889)
+// The reference's recursive build_tree is evaluated here iteratively: leaves
+// are integrated in trajectory order and a completed subtree is merged with
+// the stored left sibling of its level, which performs the merges (and their
+// random draws) in exactly the recursion's post-order. A truncated left
+// subtree (s' = false) ends the build without a merge, a truncated right
+// subtree still merges -- again as the recursion does.
+//
+// One lane group (LPC lanes x E coordinates) owns one chain; chains follow
+// their own control flow. The per-level stack of stored left subtrees lives in
+// global memory laid out [level][field][chain][coordinate]; every lane only
+// ever reads back what it wrote itself, so no cross-lane ordering is needed.
+#include "gm_layouts.h"
+#include "gm_nuts.h"
+
+namespace gm {
+
+struct NutsLaunch {
+  void* q = nullptr;
+  long long* accepts = nullptr;
+  long long* n_leapfrog = nullptr;
+  void* samples = nullptr;
+  void* eps = nullptr;
+  void* eps_bar = nullptr;
+  void* h_bar = nullptr;
+  void* mu = nullptr;
+  void* stk_vec = nullptr;
+  void* stk_alpha = nullptr;
+  int* stk_n = nullptr;
+  int* stk_na = nullptr;
+  long long C = 0;
+  int D = 0;
+  int max_depth = 10;
+  double target_accept = 0.8;
+  uint64_t seed = 0;
+  uint64_t step0 = 0;        // global transition index of this launch's first step
+  uint64_t init_step = 0;    // transition counter value used for the init draw
+  uint32_t chain_offset = 0;
+  int n_steps = 0;
+  long long m0 = 0;          // adaptation counter before this launch's first step
+  long long n_discard = 0;
+  int do_init = 0;           // run init_chain_state first (generic_nuts.rs:731-753)
+  long long t0 = 0;          // transitions already done in this run before this launch
+  long long row_shift = 0;   // state after t transitions goes to row t - row_shift
+  long long n_rows = 0;
+};
+
+template <int LPC, int E, class T>
+__device__ __forceinline__ T dot_group(const T (&a)[E], const T (&b)[E]) {
+  T part = a[0] * b[0];
+#pragma unroll
+  for (int e = 1; e < E; ++e) part = part + a[e] * b[e];
+  return group_sum<LPC>(part);
+}
+
+// MassMatrix::kinetic, identity (generic_nuts.rs:230-238): 0.5 * sum p^2
+template <int LPC, int E, class T>
+__device__ __forceinline__ T kinetic(const T (&p)[E]) {
+  return (T)0.5 * dot_group<LPC, E>(p, p);
+}
+
+// leapfrog_with_mass, identity (generic_nuts.rs:1396-1418)
+template <int LPC, int E, class T, class TG>
+__device__ __forceinline__ T leapfrog(const TG& tg, T (&q)[E], T (&p)[E], T (&g)[E], T epsv, int lane) {
+  const T h = epsv * (T)0.5;
+#pragma unroll
+  for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
+#pragma unroll
+  for (int e = 0; e < E; ++e) q[e] = q[e] + p[e] * epsv;
+  const T lp = tg.template eval<LPC, E, true>(q, g, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
+  return lp;
+}
+
+// stop_criterion (generic_nuts.rs:1354-1378), identity mass:
+// (q+ - q-) . p- >= 0  and  (q+ - q-) . p+ >= 0
+template <int LPC, int E, class T>
+__device__ __forceinline__ bool no_uturn(const T (&qm)[E], const T (&qp)[E], const T (&pm)[E],
+                                         const T (&pp)[E]) {
+  T d[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) d[e] = qp[e] - qm[e];
+  const T dm = dot_group<LPC, E>(d, pm);
+  const T dp = dot_group<LPC, E>(d, pp);
+  return dm >= (T)0 && dp >= (T)0;
+}
+
+template <int LPC, class T>
+__device__ __forceinline__ bool all_finite(const T (&x)[1]) { return true; }
+
+template <int LPC, int E, class T>
+__device__ __forceinline__ bool group_all_finite(const T (&x)[E], int lane, int D) {
+  int bad = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    const T v = x[e];
+    if (i < D && !(v - v == (T)0)) bad = 1;  // inf - inf and NaN - NaN are NaN
+  }
+  return group_sum<LPC>(bad) == 0;
+}
+
+template <class T> __device__ __forceinline__ T rust_min1(T x) {  // T::one().min(x)
+  if (x != x) return (T)1;
+  return x < (T)1 ? x : (T)1;
+}
+
+template <class T> struct MachEps;
+template <> struct MachEps<float> { static constexpr float v = 1.1920928955078125e-07f; };
+template <> struct MachEps<double> { static constexpr double v = 2.220446049250313e-16; };
+
+// find_reasonable_epsilon_with_mass (generic_nuts.rs:1025-1102), identity mass.
+template <int LPC, int E, class T, class TG>
+__device__ T find_reasonable_epsilon(const TG& tg, const T (&q0)[E], const T (&p0)[E], int lane, int D) {
+  const T half = (T)0.5;
+  T eps = (T)1;
+  T g0[E];
+  const T ulogp = tg.template eval<LPC, E, true>(q0, g0, lane);
+  T q[E], p[E], g[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) { q[e] = q0[e]; p[e] = p0[e]; g[e] = g0[e]; }
+  T ulogp1 = leapfrog<LPC, E>(tg, q, p, g, eps, lane);
+  T k = (T)1;
+  for (int it = 0; it < 1100; ++it) {  // bounded: k underflows to 0 long before
+    const bool fin = (ulogp1 - ulogp1 == (T)0) && group_all_finite<LPC, E>(g, lane, D);
+    if (fin) break;
+    k = k * half;
+#pragma unroll
+    for (int e = 0; e < E; ++e) { q[e] = q0[e]; p[e] = p0[e]; g[e] = g0[e]; }
+    ulogp1 = leapfrog<LPC, E>(tg, q, p, g, eps * k, lane);
+  }
+  eps = half * k * eps;
+  const T k0 = kinetic<LPC, E>(p0);
+  T la = ulogp1 - ulogp - (kinetic<LPC, E>(p) - k0);
+  const T a = (la > glog(half)) ? (T)1 : (T)-1;
+  const T ln2 = glog((T)2);
+  for (int it = 0; it < 2200; ++it) {  // bounded (the reference is not)
+    if (!(a * la > -a * ln2)) break;
+    eps = eps * (a > (T)0 ? (T)2 : (T)0.5);  // 2^a, a = +-1
+#pragma unroll
+    for (int e = 0; e < E; ++e) { q[e] = q0[e]; p[e] = p0[e]; g[e] = g0[e]; }
+    ulogp1 = leapfrog<LPC, E>(tg, q, p, g, eps, lane);
+    la = ulogp1 - ulogp - (kinetic<LPC, E>(p) - k0);
+  }
+  return eps;
+}
+
+template <class T, int LPC, int E, class TG>
+__global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg) {
+  const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long c = gtid / LPC;
+  const int lane = (int)(gtid % LPC);
+  if (c >= a.C) return;
+  const int D = a.D;
+  const long long C = a.C;
+  const uint32_t cid = a.chain_offset + (uint32_t)c;
+  T* __restrict__ qs = (T*)a.q;
+  T* __restrict__ svec = (T*)a.stk_vec;
+  T* __restrict__ salpha = (T*)a.stk_alpha;
+  const long long slane = c * LPC + lane;  // scalar-stack slot of this lane
+  const long long CL = C * LPC;
+
+  T q[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    q[e] = (i < D) ? qs[c * D + i] : (T)0;
+  }
+  T eps = ((T*)a.eps)[c], eps_bar = ((T*)a.eps_bar)[c], h_bar = ((T*)a.h_bar)[c], mu = ((T*)a.mu)[c];
+  const T gamma = (T)0.05, kappa = (T)0.75, delta = (T)a.target_accept;
+  const long long t0c = 10;
+
+  if (a.do_init) {  // init_chain_state (generic_nuts.rs:731-753)
+    T p0[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      p0[e] = (i < D) ? normal<T>(a.seed, cid, a.init_step, TAG_NUTS_INIT, (uint32_t)i) : (T)0;
+    }
+    const T ae = eps + (T)1;
+    if ((ae < (T)0 ? -ae : ae) <= MachEps<T>::v) eps = find_reasonable_epsilon<LPC, E>(tg, q, p0, lane, D);
+    mu = glog((T)10 * eps);
+  }
+  auto record = [&](long long t) {
+    const long long row = t - a.row_shift;
+    if (row >= 0 && row < a.n_rows) {
+      T* __restrict__ out = (T*)a.samples + (row * C + c) * D;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        if (i < D) out[i] = q[e];
+      }
+    }
+  };
+  if (a.t0 == 0) record(0);
+
+  long long acc = 0, nlf = 0;
+  for (int s = 0; s < a.n_steps; ++s) {
+    const uint64_t st = a.step0 + (uint64_t)s;
+    const long long m = a.m0 + s + 1;
+    // --- momentum, slice (generic_nuts.rs:758-768)
+    T p0[E], g0[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      p0[e] = (i < D) ? normal<T>(a.seed, cid, st, TAG_NUTS_MOM, (uint32_t)i) : (T)0;
+    }
+    const T logp0 = tg.template eval<LPC, E, true>(q, g0, lane);
+    const T joint0 = logp0 - kinetic<LPC, E>(p0);
+    const T logu = joint0 - exp1<T>(a.seed, cid, st, TAG_NUTS_EXP, 0u);
+    // trajectory ends
+    T qm[E], pm[E], gm_[E], qp[E], pp[E], gp[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      qm[e] = q[e]; qp[e] = q[e];
+      pm[e] = p0[e]; pp[e] = p0[e];
+      gm_[e] = g0[e]; gp[e] = g0[e];
+    }
+    long long n = 1;
+    bool s_ok = true;
+    T alpha = (T)0;
+    long long n_alpha = 0;
+    uint32_t merge_ctr = 0;
+    int j = 0;
+    while (s_ok && j < a.max_depth) {
+      const T u1 = uniform_co<T>(a.seed, cid, st, TAG_NUTS_DIR, (uint32_t)j);
+      const int v = (u1 < (T)0.5) ? 1 : -1;
+      const T epsv = (T)v * eps;
+      // edge state = the trajectory end on side v
+      T qe[E], pe[E], ge[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        qe[e] = v > 0 ? qp[e] : qm[e];
+        pe[e] = v > 0 ? pp[e] : pm[e];
+        ge[e] = v > 0 ? gp[e] : gm_[e];
+      }
+      // current subtree T
+      T fq[E], fp[E], pr[E];
+      long long tn = 0;
+      bool ts = true;
+      T ta = (T)0;
+      long long tna = 0;
+      const long long nleaves = 1LL << j;
+      for (long long l = 0; l < nleaves; ++l) {
+        const T lp = leapfrog<LPC, E>(tg, qe, pe, ge, epsv, lane);
+        ++nlf;
+        const T joint = lp - kinetic<LPC, E>(pe);
+        tn = (logu < joint) ? 1 : 0;
+        ts = (logu - (T)1000) < joint;
+        ta = rust_min1(gexp(joint - joint0));
+        tna = 1;
+#pragma unroll
+        for (int e = 0; e < E; ++e) { fq[e] = qe[e]; fp[e] = pe[e]; pr[e] = qe[e]; }
+        bool done = false;
+        int k = 0;
+        while (true) {
+          if (k == j) { done = true; break; }
+          if (((l >> k) & 1) == 0) {  // left child at level k
+            if (!ts) { done = true; break; }
+            T* sv = svec + ((long long)(k * 3) * C + c) * D;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+              const int i = lane * E + e;
+              if (i < D) {
+                sv[i] = fq[e];
+                sv[C * D + i] = fp[e];
+                sv[2 * C * D + i] = pr[e];
+              }
+            }
+            salpha[k * CL + slane] = ta;
+            a.stk_n[k * CL + slane] = (int)tn;
+            a.stk_na[k * CL + slane] = (int)tna;
+            break;
+          }
+          // right child: merge with the stored left sibling (generic_nuts.rs:1251-1323)
+          const T* sv = svec + ((long long)(k * 3) * C + c) * D;
+          T lq[E], lpv[E];
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const int i = lane * E + e;
+            lq[e] = (i < D) ? sv[i] : (T)0;
+            lpv[e] = (i < D) ? sv[C * D + i] : (T)0;
+          }
+          const long long ln_ = a.stk_n[k * CL + slane];
+          const long long lna = a.stk_na[k * CL + slane];
+          const T lal = salpha[k * CL + slane];
+          const double u = uniform_co<double>(a.seed, cid, st, TAG_NUTS_MRG, merge_ctr++);
+          const long long den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
+          if (!(u < (double)tn / (double)den)) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+              const int i = lane * E + e;
+              pr[e] = (i < D) ? sv[2 * C * D + i] : (T)0;
+            }
+          }
+          tn = ln_ + tn;
+          if (ts) ts = (v > 0) ? no_uturn<LPC, E>(lq, qe, lpv, pe) : no_uturn<LPC, E>(qe, lq, pe, lpv);
+          ta = lal + ta;
+          tna = lna + tna;
+#pragma unroll
+          for (int e = 0; e < E; ++e) { fq[e] = lq[e]; fp[e] = lpv[e]; }
+          ++k;
+        }
+        if (done) break;
+      }
+      // the new trajectory end on side v is the last leaf integrated
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (v > 0) { qp[e] = qe[e]; pp[e] = pe[e]; gp[e] = ge[e]; }
+        else { qm[e] = qe[e]; pm[e] = pe[e]; gm_[e] = ge[e]; }
+      }
+      alpha = ta;
+      n_alpha = tna;
+      const T tmp = rust_min1((T)tn / (T)n);
+      const T u2 = uniform_co<T>(a.seed, cid, st, TAG_NUTS_TOP, (uint32_t)j);
+      if (ts && (u2 < tmp)) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) q[e] = pr[e];
+        ++acc;
+      }
+      n += tn;
+      s_ok = ts && no_uturn<LPC, E>(qm, qp, pm, pp);
+      ++j;
+    }
+    // dual averaging (generic_nuts.rs:882-924)
+    T eta = (T)1 / (T)(m + t0c);
+    h_bar = ((T)1 - eta) * h_bar + eta * (delta - alpha / (T)n_alpha);
+    if (m <= a.n_discard) {
+      const T mf = (T)m;
+      eps = gexp(mu - gsqrt(mf) / gamma * h_bar);
+      eta = gexp(-kappa * glog(mf));  // m^(-kappa)
+      eps_bar = gexp(((T)1 - eta) * glog(eps_bar) + eta * glog(eps));
+    } else {
+      eps = eps_bar;
+    }
+    record(a.t0 + s + 1);
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    if (i < D) qs[c * D + i] = q[e];
+  }
+  if (lane == 0) {
+    ((T*)a.eps)[c] = eps;
+    ((T*)a.eps_bar)[c] = eps_bar;
+    ((T*)a.h_bar)[c] = h_bar;
+    ((T*)a.mu)[c] = mu;
+    a.accepts[c] += acc;
+    a.n_leapfrog[c] += nlf;
+  }
+}
+
+template <class T>
+__global__ void nuts_fill_kernel(T* eps, T* eps_bar, T* h_bar, T* mu, long long C) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= C) return;
+  eps[i] = (T)-1;                   // generic_nuts.rs:619
+  eps_bar[i] = (T)1;                // :645
+  h_bar[i] = (T)0;                  // :646
+  mu[i] = glog((T)10 * (T)1);       // :644
+}
+
+int nuts_init_state(NutsState* ns, gm_dtype dt, long long C, int D, int max_depth) {
+  const size_t esz = dt == GM_F32 ? 4 : 8;
+  ns->max_depth = max_depth;
+  hipError_t e = hipSuccess;
+  e = hipMalloc(&ns->eps, C * esz);
+  if (e == hipSuccess) e = hipMalloc(&ns->eps_bar, C * esz);
+  if (e == hipSuccess) e = hipMalloc(&ns->h_bar, C * esz);
+  if (e == hipSuccess) e = hipMalloc(&ns->mu, C * esz);
+  if (e == hipSuccess) e = hipMalloc((void**)&ns->n_leapfrog, C * sizeof(long long));
+  if (e == hipSuccess && max_depth > 0)
+    e = hipMalloc(&ns->stk_vec, (size_t)max_depth * 3 * C * D * esz);
+  if (e != hipSuccess) {
+    set_error(std::string("NUTS state allocation failed: ") + hipGetErrorString(e));
+    return GM_ENOMEM;
+  }
+  hipMemset(ns->n_leapfrog, 0, C * sizeof(long long));
+  const unsigned blocks = (unsigned)((C + 255) / 256);
+  if (dt == GM_F32)
+    hipLaunchKernelGGL(nuts_fill_kernel<float>, dim3(blocks), dim3(256), 0, 0, (float*)ns->eps,
+                       (float*)ns->eps_bar, (float*)ns->h_bar, (float*)ns->mu, C);
+  else
+    hipLaunchKernelGGL(nuts_fill_kernel<double>, dim3(blocks), dim3(256), 0, 0, (double*)ns->eps,
+                       (double*)ns->eps_bar, (double*)ns->h_bar, (double*)ns->mu, C);
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) {
+    set_error(std::string("NUTS state init failed: ") + hipGetErrorString(e));
+    return GM_EHIP;
+  }
+  ns->inited = true;
+  return GM_OK;
+}
+
+static void ffree(void* p) {
+  if (p) hipFree(p);
+}
+
+void nuts_free_state(NutsState* ns) {
+  ffree(ns->eps);
+  ffree(ns->eps_bar);
+  ffree(ns->h_bar);
+  ffree(ns->mu);
+  ffree(ns->stk_vec);
+  ffree(ns->stk_alpha);
+  ffree(ns->stk_n);
+  ffree(ns->stk_na);
+  ffree(ns->n_leapfrog);
+  *ns = NutsState();
+}
+
+int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay, void* q,
+             long long* accepts, void* samples, long long C, int D, double target_accept,
+             uint64_t seed, uint64_t* step, uint32_t chain_offset, long long total,
+             long long n_discard, int progress, long long steps_per_launch, hipStream_t st,
+             std::vector<hipEvent_t>& evs, double* ms, long long* launches) {
+  const size_t esz = dt == GM_F32 ? 4 : 8;
+  // scalar stack is per lane; (re)size for the current layout
+  const long long lanes_total = C * lay.lanes;
+  if (ns.stk_lanes != lanes_total && ns.max_depth > 0) {
+    ffree(ns.stk_alpha);
+    ffree(ns.stk_n);
+    ffree(ns.stk_na);
+    ns.stk_alpha = nullptr;
+    ns.stk_n = ns.stk_na = nullptr;
+    hipError_t e = hipMalloc(&ns.stk_alpha, (size_t)ns.max_depth * lanes_total * esz);
+    if (e == hipSuccess) e = hipMalloc((void**)&ns.stk_n, (size_t)ns.max_depth * lanes_total * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc((void**)&ns.stk_na, (size_t)ns.max_depth * lanes_total * sizeof(int));
+    if (e != hipSuccess) {
+      set_error("NUTS stack allocation failed");
+      return GM_ENOMEM;
+    }
+    ns.stk_lanes = lanes_total;
+  }
+  // init_chain_state at the start of every run (generic_nuts.rs:731-753)
+  ns.m = 0;
+  ns.n_discard = n_discard;
+  const uint64_t init_step = *step;
+  const long long n_rows_total = progress ? total - n_discard : total - n_discard + 1;
+  const long long row_shift = progress ? n_discard + 1 : n_discard;
+  const long long chunk = steps_per_launch;
+  long long n_launch = (total + chunk - 1) / chunk;
+  if (n_launch == 0) n_launch = 1;  // run with zero transitions still records row 0
+  while ((long long)evs.size() < 2 * n_launch) {
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) {
+      set_error("hipEventCreate failed");
+      return GM_EHIP;
+    }
+    evs.push_back(ev);
+  }
+  long long li = 0;
+  for (long long start = 0; li < n_launch; start += chunk, ++li) {
+    long long nst = total - start < chunk ? total - start : chunk;
+    if (nst < 0) nst = 0;
+    NutsLaunch a;
+    a.q = q;
+    a.accepts = accepts;
+    a.n_leapfrog = ns.n_leapfrog;
+    a.samples = samples;
+    a.eps = ns.eps;
+    a.eps_bar = ns.eps_bar;
+    a.h_bar = ns.h_bar;
+    a.mu = ns.mu;
+    a.stk_vec = ns.stk_vec;
+    a.stk_alpha = ns.stk_alpha;
+    a.stk_n = ns.stk_n;
+    a.stk_na = ns.stk_na;
+    a.C = C;
+    a.D = D;
+    a.max_depth = ns.max_depth;
+    a.target_accept = target_accept;
+    a.seed = seed;
+    a.step0 = *step + start;
+    a.init_step = init_step;
+    a.chain_offset = chain_offset;
+    a.n_steps = (int)nst;
+    a.m0 = ns.m + start;
+    a.n_discard = n_discard;
+    a.do_init = (start == 0) ? 1 : 0;
+    a.t0 = start;
+    a.row_shift = row_shift;
+    a.n_rows = n_rows_total > 0 ? n_rows_total : 0;
+    hipEventRecord(evs[2 * li], st);
+    hipError_t e = dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
+      const long long threads = C * LPC;
+      const unsigned blocks = (unsigned)((threads + 255) / 256);
+      hipLaunchKernelGGL((nuts_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), 0, st, a, t);
+      return hipGetLastError();
+    });
+    if (e != hipSuccess) {
+      set_error(std::string("NUTS launch failed: ") + hipGetErrorString(e));
+      return GM_EHIP;
+    }
+    hipEventRecord(evs[2 * li + 1], st);
+  }
+  ns.m += total;
+  *step += (uint64_t)total + 1;  // +1: the init draw consumed a counter value
+  hipError_t e = hipStreamSynchronize(st);
+  if (e != hipSuccess) {
+    set_error(std::string("NUTS run failed: ") + hipGetErrorString(e));
+    return GM_EHIP;
+  }
+  double tot = 0;
+  for (long long i = 0; i < n_launch; ++i) {
+    float t = 0;
+    hipEventElapsedTime(&t, evs[2 * i], evs[2 * i + 1]);
+    tot += t;
+  }
+  *ms = tot;
+  *launches = n_launch;
+  return GM_OK;
+}
+
+int nuts_get_step_size(NutsState& ns, gm_dtype dt, long long C, double* eps, double* eps_bar) {
+  const size_t esz = dt == GM_F32 ? 4 : 8;
+  std::vector<unsigned char> b1(C * esz), b2(C * esz);
+  if (hipMemcpy(b1.data(), ns.eps, C * esz, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(b2.data(), ns.eps_bar, C * esz, hipMemcpyDeviceToHost) != hipSuccess) {
+    set_error("copy of NUTS step sizes failed");
+    return GM_EHIP;
+  }
+  for (long long i = 0; i < C; ++i) {
+    if (dt == GM_F32) {
+      if (eps) eps[i] = ((float*)b1.data())[i];
+      if (eps_bar) eps_bar[i] = ((float*)b2.data())[i];
+    } else {
+      if (eps) eps[i] = ((double*)b1.data())[i];
+      if (eps_bar) eps_bar[i] = ((double*)b2.data())[i];
+    }
+  }
+  return GM_OK;
+}
+
+int nuts_get_leapfrogs(NutsState& ns, long long C, long long* out) {
+  if (hipMemcpy(out, ns.n_leapfrog, C * sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess) {
+    set_error("copy of NUTS leapfrog counts failed");
+    return GM_EHIP;
+  }
+  return GM_OK;
+}
+
+}  // namespace gm

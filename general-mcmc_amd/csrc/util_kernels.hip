@@ -1,0 +1,74 @@
+// util_kernels.hip — target evaluation (logp_and_grad over a batch of
+// points, batched_hmc.rs:18-22 / hmc.rs:42-61) and the sample-layout
+// transpose used on egress ([N][C][D] device -> [C][N][D] reference layout,
+// hmc.rs:179-180).
+#include "gm_layouts.h"
+
+namespace gm {
+
+template <class T, int LPC, int E, class TG>
+__global__ __launch_bounds__(256) void logp_grad_kernel(long long n, int D, const T* __restrict__ x,
+                                                        T* __restrict__ logp, T* __restrict__ grad,
+                                                        TG tg) {
+  const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long c = gtid / LPC;
+  const int lane = (int)(gtid % LPC);
+  if (c >= n) return;
+  T q[E], g[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    q[e] = (i < D) ? x[c * D + i] : (T)0;
+  }
+  const T lp = tg.template eval<LPC, E, true>(q, g, lane);
+  if (grad) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      if (i < D) grad[c * D + i] = g[e];
+    }
+  }
+  if (lane == 0 && logp) logp[c] = lp;
+}
+
+hipError_t launch_logp_grad(gm_dtype dt, const TargetDev& tg, const Layout& lay, long long n,
+                            const void* x, void* logp, void* grad, hipStream_t st) {
+  return dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
+    const long long threads = n * LPC;
+    const unsigned blocks = (unsigned)((threads + 255) / 256);
+    hipLaunchKernelGGL((logp_grad_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), 0, st, n,
+                       tg.D, (const T*)x, (T*)logp, (T*)grad, t);
+    return hipGetLastError();
+  });
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ src, T* __restrict__ dst,
+                                                        long long rows, long long C, long long D) {
+  const long long total = rows * C * D;
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+       k += (long long)gridDim.x * blockDim.x) {
+    const long long d = k % D;
+    const long long rc = k / D;       // = c*rows + r in dst order
+    const long long r = rc % rows;
+    const long long c = rc / rows;
+    dst[k] = src[(r * C + c) * D + d];
+  }
+}
+
+hipError_t launch_transpose_samples(gm_dtype dt, const void* src, void* dst, long long rows,
+                                    long long C, long long D, hipStream_t st) {
+  const long long total = rows * C * D;
+  if (total == 0) return hipSuccess;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  if (dt == GM_F32)
+    hipLaunchKernelGGL(transpose_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, st,
+                       (const float*)src, (float*)dst, rows, C, D);
+  else
+    hipLaunchKernelGGL(transpose_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, st,
+                       (const double*)src, (double*)dst, rows, C, D);
+  return hipGetLastError();
+}
+
+}  // namespace gm

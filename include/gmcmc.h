@@ -1,0 +1,229 @@
+/*
+ * gmcmc.h — C ABI of the MI355X many-chain HMC / NUTS / Metropolis-Hastings
+ * engine (libgmcmc.so, HIP kernels for gfx950).
+ *
+ * This is the drop-in boundary for the hot path of SauersML/general-mcmc
+ * (reference snapshot under /root/reference). Each entry point names the
+ * reference interface it replaces. Plain pointers and sizes only; no torch
+ * types. All functions return GM_OK (0) or an error code; the message of the
+ * last error on the calling thread is available from gm_last_error(). No
+ * function aborts the process: the reference's panics (shape asserts,
+ * euclidean.rs:116-120/432-437, distributions.rs:267) become GM_EINVAL.
+ *
+ * Data layout conventions
+ *   - host initial positions / host outputs are row-major, reference layout:
+ *     init [n_chains][dim]           (hmc.rs:119-124, Vec<Vec<T>> flattened)
+ *     samples [n_chains][n_collect][dim] (hmc.rs:179-180 stack+permute)
+ *   - device-resident samples (gm_*_run_device) are [n_collect][n_chains][dim]
+ *     (one contiguous [C,D] slab per collected step, as BatchedGenericHMC::
+ *     run_positions returns one Tensor<B,2> per step, batched_hmc.rs:115-123).
+ *   - element type is given by gm_dtype (f32 or f64) everywhere.
+ *
+ * Threading: one sampler must not be used from two threads at once
+ * (&mut self in the reference, hmc.rs:164). Distinct samplers may run
+ * concurrently; each owns a HIP stream on the device that was current
+ * (gm_set_device) when it was created.
+ */
+#ifndef GMCMC_H
+#define GMCMC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+#define GM_OK 0
+#define GM_EINVAL 1 /* bad argument / shape (reference: assert_eq!/expect panics) */
+#define GM_EHIP 2   /* HIP runtime error */
+#define GM_ENOMEM 3 /* device allocation failed */
+#define GM_ERCCL 4  /* RCCL error */
+#define GM_ESTATE 5 /* call not valid in the sampler's current state */
+
+typedef enum gm_dtype { GM_F32 = 0, GM_F64 = 1 } gm_dtype;
+
+/* ---- targets (replaces the user-implemented traits) ---------------------
+ * BatchedGradientTarget::unnorm_logp_batch   distributions.rs:67-78
+ * GradientTarget::unnorm_logp(+_and_grad)     distributions.rs:80-90
+ * Target::unnorm_logp                         distributions.rs:107-110
+ * Built-in targets get analytic gradients instead of burn autodiff
+ * (hmc.rs:42-61).                                                          */
+typedef enum gm_target_kind {
+  GM_TARGET_ROSENBROCK = 1, /* RosenbrockND (a=1,b=100) distributions.rs:535-555;
+                               Rosenbrock2D{a,b} distributions.rs:495-530    */
+  GM_TARGET_ISO_GAUSS = 2,  /* IsotropicGaussian as Target, distributions.rs:398-406 */
+  GM_TARGET_GAUSS = 3       /* DiffableGaussian2D distributions.rs:215-320 generalised
+                               to D dims: logp = norm_const - 0.5 (x-mu)^T P (x-mu),
+                               P = Sigma^-1 supplied row-major; also Gaussian2D as a
+                               Target (distributions.rs:193-207) with norm_const = 0 */
+} gm_target_kind;
+
+typedef struct gm_target {
+  int32_t kind;          /* gm_target_kind */
+  int32_t reserved;
+  int64_t dim;           /* must equal the sampler's dim */
+  double a, b;           /* ROSENBROCK: logp = -sum_i [ b (x_{i+1}-x_i^2)^2 + (a-x_i)^2 ] */
+  double std;            /* ISO_GAUSS: logp = -0.5 * sum x^2 / std^2 */
+  const double* mean;    /* GAUSS: [dim] */
+  const double* prec;    /* GAUSS: [dim*dim] row-major inverse covariance */
+  double norm_const;     /* GAUSS: additive constant */
+} gm_target;
+
+/* DiffableGaussian2D::new (distributions.rs:229-253) generalised: from a mean
+ * and covariance compute the precision matrix and norm_const =
+ * -(dim ln(2 pi) + ln|Sigma|)/2. For dim == 2 the closed-form 2x2 inverse of
+ * the reference is used bit-for-bit; otherwise a Cholesky factorisation. */
+int gm_gauss_from_cov(int64_t dim, const double* cov, double* prec_out, double* norm_const_out);
+
+/* Evaluate a target on host-provided points (device compute): logp [n],
+ * grad [n][dim] (grad may be NULL). Replaces logp_and_grad
+ * (batched_hmc.rs:18-22, hmc.rs:42-61). */
+int gm_target_logp_grad(const gm_target* target, gm_dtype dtype, int64_t n, const void* x,
+                        void* logp_out, void* grad_out);
+
+/* Initial positions: n x dim iid N(0,1) from the engine's counter-based
+ * stream keyed by `seed` (core.rs:434-475 init / init_det / init_with_seed
+ * analogue: same distribution and row-by-row meaning, not the same numbers,
+ * see gm_rng.h). Host-side; out is [n][dim] of dtype. */
+int gm_init_positions(uint64_t seed, int64_t n, int64_t dim, gm_dtype dtype, void* out);
+
+/* ---- device / errors ------------------------------------------------ */
+const char* gm_last_error(void);
+int gm_device_count(int* count);
+int gm_set_device(int device);
+int gm_device_synchronize(void);
+
+/* ---- samplers ----------------------------------------------------------- */
+typedef struct gm_sampler gm_sampler;
+
+/* HMC::new (hmc.rs:113-134) / BatchedGenericHMC::new (batched_hmc.rs:62-84).
+ * init: host [n_chains][dim] of dtype. chain_offset: global id of chain 0
+ * (used to key the per-chain random streams; 0 unless chains are sharded
+ * across processes/GPUs). */
+int gm_hmc_create(const gm_target* target, gm_dtype dtype, int64_t n_chains, int64_t dim,
+                  const void* init, double step_size, int64_t n_leapfrog,
+                  int64_t chain_offset, gm_sampler** out);
+
+/* MetropolisHastings::new (metropolis_hastings.rs:151-161) with an
+ * IsotropicGaussian proposal of standard deviation proposal_std
+ * (distributions.rs:349-390), driven like ChainRunner::run (core.rs:219-229). */
+int gm_mh_create(const gm_target* target, gm_dtype dtype, int64_t n_chains, int64_t dim,
+                 const void* init, double proposal_std, int64_t chain_offset,
+                 gm_sampler** out);
+
+/* NUTS::new (nuts.rs:156-180) -> GenericNUTS::new (generic_nuts.rs:370-377):
+ * identity mass matrix, dual-averaging step size (gamma .05, t0 10, kappa .75).
+ * max_depth bounds the doubling loop (the reference has no bound,
+ * generic_nuts.rs:782); pass 0 for the engine default (10). */
+int gm_nuts_create(const gm_target* target, gm_dtype dtype, int64_t n_chains, int64_t dim,
+                   const void* init, double target_accept_p, int32_t max_depth,
+                   int64_t chain_offset, gm_sampler** out);
+
+/* set_seed: hmc.rs:143-148, generic_nuts.rs:550-556, metropolis_hastings.rs:189-197.
+ * Resets the sampler's transition counter so a re-seeded sampler replays. */
+int gm_set_seed(gm_sampler* s, uint64_t seed);
+
+/* One transition of every chain (HMC::step hmc.rs:316-318 /
+ * BatchedGenericHMC::step batched_hmc.rs:129-163 / MHMarkovChain::step
+ * metropolis_hastings.rs:306-318 / GenericNUTSChain::step generic_nuts.rs:755-925). */
+int gm_step(gm_sampler* s);
+
+/* run(n_collect, n_discard): hmc.rs:164-181, core.rs:219-229, nuts.rs:214-259.
+ * out: host [n_chains][n_collect][dim] (may be NULL to skip the copy).
+ * Step-count semantics follow the reference per sampler kind:
+ *   HMC, MH: n_discard + n_collect transitions, every post-burn-in state kept;
+ *   NUTS:    n_discard + n_collect - 1 transitions, row r = state after
+ *            n_discard + r transitions (row 0 = start when n_discard == 0). */
+int gm_run(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out);
+
+/* run_positions (batched_hmc.rs:115-123): same transitions, samples stay on
+ * the device as [n_collect][n_chains][dim]; *dev_samples is owned by the
+ * sampler and valid until the next run/destroy. */
+int gm_run_device(gm_sampler* s, int64_t n_collect, int64_t n_discard, const void** dev_samples);
+
+/* NUTS::run_progress semantics (generic_nuts.rs:675-717): n_discard + n_collect
+ * transitions, row r = state after n_discard + r + 1 transitions. Other
+ * sampler kinds: identical to gm_run_device. */
+int gm_run_device_progress(gm_sampler* s, int64_t n_collect, int64_t n_discard,
+                           const void** dev_samples);
+
+/* run_progress (hmc.rs:245-306, generic_nuts.rs:414-548, core.rs:251-403)
+ * without the terminal UI: the transitions of gm_run_device_progress, samples
+ * copied to host [n_chains][n_collect][dim] (out may be NULL), and the
+ * device-side split R-hat / ESS of the collected draws (RunStats::from,
+ * stats.rs:383-394) in rhat_out/ess_out [dim] (may be NULL; needs n_collect >= 2). */
+int gm_run_progress(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out,
+                    float* rhat_out, float* ess_out);
+
+/* Copy the samples of the last run (device [n_collect][n_chains][dim]) to host
+ * in the reference layout [n_chains][n_collect][dim]. */
+int gm_copy_samples(gm_sampler* s, void* out);
+
+/* positions() (hmc.rs:326-328): host [n_chains][dim]. */
+int gm_get_positions(gm_sampler* s, void* out);
+int gm_set_positions(gm_sampler* s, const void* in);
+
+/* Per-chain count of accepted transitions since creation / set_seed
+ * (the quantity behind MultiChainTracker::p_accept, stats.rs:238-269). */
+int gm_get_accept_counts(gm_sampler* s, int64_t* out);
+
+/* Per-chain count of leapfrog steps integrated since creation (HMC:
+ * n_leapfrog per transition; NUTS: the tree sizes actually built; MH: 0). */
+int gm_get_leapfrog_counts(gm_sampler* s, int64_t* out);
+
+/* NUTS per-chain adaptation state: step size epsilon and epsilon_bar
+ * (generic_nuts.rs:573-582). Pass NULL to skip either. */
+int gm_nuts_get_step_size(gm_sampler* s, double* eps, double* eps_bar);
+
+/* Lane layout the kernels use for this sampler: `lanes` lanes cooperate on
+ * one chain, each holding `elems` consecutive coordinates. Per-chain sums
+ * (kinetic energy, log-density) are reduced lane-sequentially then by an xor
+ * butterfly over the lanes, which fixes the floating-point summation order. */
+int gm_sampler_layout(gm_sampler* s, int32_t* lanes, int32_t* elems);
+int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems);
+
+/* Device time (ms) of the sampling kernels launched by the last run, and the
+ * number of launches (HIP events on the sampler's stream). */
+int gm_sampler_last_run_stats(gm_sampler* s, double* kernel_ms, int64_t* launches);
+
+/* Transitions per kernel launch (state stays in registers inside a launch). */
+int gm_sampler_set_steps_per_launch(gm_sampler* s, int64_t steps);
+
+int gm_destroy(gm_sampler* s);
+
+/* ---- diagnostics (stats.rs) ---------------------------------------------
+ * split_rhat_mean_ess (stats.rs:439-450, Appendix B of SURVEY.md): returns
+ * split R-hat = sqrt(W/V) (the reference's orientation, stats.rs:452-454) and
+ * ESS per parameter, as f32, like the reference.
+ * Host variant: sample is host [n_chains][n_draws][n_params] (reference
+ * layout). Device variant: sample is a device pointer with explicit element
+ * strides (chain, draw, param). */
+int gm_split_rhat_ess(const void* sample, gm_dtype dtype, int64_t n_chains, int64_t n_draws,
+                      int64_t n_params, float* rhat_out, float* ess_out);
+int gm_split_rhat_ess_device(const void* dev_sample, gm_dtype dtype, int64_t n_chains,
+                             int64_t n_draws, int64_t n_params, int64_t stride_chain,
+                             int64_t stride_draw, int64_t stride_param, float* rhat_out,
+                             float* ess_out);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) -------------------
+ * Chains are sharded in contiguous blocks; sampling needs no communication.
+ * The only exchange is an RCCL all-gather of per-split-chain summaries for
+ * split-R-hat/ESS. */
+typedef struct gm_comm gm_comm;
+#define GM_UNIQUE_ID_BYTES 128
+int gm_comm_get_unique_id(void* id_out /* GM_UNIQUE_ID_BYTES */);
+int gm_comm_init(const void* id, int32_t nranks, int32_t rank, gm_comm** out);
+int gm_comm_destroy(gm_comm* comm);
+/* Same result on every rank: diagnostics of the union of all ranks' chains
+ * (rank r holds global chains [offset_r, offset_r + n_chains_local)). */
+int gm_split_rhat_ess_dist(gm_comm* comm, const void* dev_sample, gm_dtype dtype,
+                           int64_t n_chains_local, int64_t n_draws, int64_t n_params,
+                           int64_t stride_chain, int64_t stride_draw, int64_t stride_param,
+                           float* rhat_out, float* ess_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GMCMC_H */

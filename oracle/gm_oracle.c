@@ -1,0 +1,532 @@
+/*
+ * gm_oracle.c — CPU ORACLE (test infrastructure only; see gm_oracle.h).
+ *
+ * Part 1: the random-number / special-function spec (restated from the
+ * engine's documentation in DESIGN.md "RNG spec": Philox4x32-10, 24/53-bit
+ * uniforms, Box-Muller cosine branch, FreeBSD-msun log/exp polynomials).
+ * Part 2 (gm_oracle_t.inc, instantiated for double and float): targets, HMC,
+ * MH, NUTS, each citing the reference lines it restates.
+ * Part 3: split-R-hat / ESS / autocovariance / MultiChainTracker (stats.rs).
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off; no -ffast-math).
+ */
+#include "gm_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+enum {
+  TAG_INIT = 1, TAG_MOM = 2, TAG_ACC = 3, TAG_MH_PROP = 4, TAG_MH_ACC = 5, TAG_NUTS_MOM = 6,
+  TAG_NUTS_EXP = 7, TAG_NUTS_DIR = 8, TAG_NUTS_TOP = 9, TAG_NUTS_MRG = 10, TAG_NUTS_INIT = 11
+};
+
+/* ===================== Part 1: RNG spec ===================== */
+void or_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static void draw(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx,
+                 uint32_t out[4]) {
+  uint32_t ctr[4] = {idx, chain, (uint32_t)step, tag | ((uint32_t)(step >> 32) << 8)};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  or_philox(ctr, key, out);
+}
+
+static uint64_t bits_d(double x) { uint64_t u; memcpy(&u, &x, 8); return u; }
+static double from_bits_d(uint64_t u) { double x; memcpy(&x, &u, 8); return x; }
+static uint32_t bits_f(float x) { uint32_t u; memcpy(&u, &x, 4); return u; }
+static float from_bits_f(uint32_t u) { float x; memcpy(&x, &u, 4); return x; }
+
+static double unif_co_d(uint32_t a, uint32_t b) {
+  uint64_t k = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+  return (double)k * 1.1102230246251565e-16;
+}
+static double unif_oc_d(uint32_t a, uint32_t b) {
+  uint64_t k = ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+  return (double)(k + 1u) * 1.1102230246251565e-16;
+}
+static float unif_co_f(uint32_t a) { return (float)(a >> 8) * 5.9604644775390625e-08f; }
+static float unif_oc_f(uint32_t a) { return (float)((a >> 8) + 1u) * 5.9604644775390625e-08f; }
+
+/* natural log: FreeBSD msun e_log.c */
+double or_log_d(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+               Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  if (x != x) return x;
+  if (x < 0.0) return from_bits_d(0x7ff8000000000000ull);
+  if (x == 0.0) return -from_bits_d(0x7ff0000000000000ull);
+  uint64_t u = bits_d(x);
+  if ((u >> 52) >= 0x7ff) return x;
+  int k = 0;
+  if ((u >> 52) == 0) { x = x * 18014398509481984.0; u = bits_d(x); k = -54; }
+  k += (int)(u >> 52) - 1023;
+  double m = from_bits_d((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+  if (m > 1.4142135623730951) { m = m * 0.5; k += 1; }
+  double f = m - 1.0;
+  double s = f / (2.0 + f);
+  double z = s * s, w = z * z;
+  double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  double R = t2 + t1;
+  double hfsq = 0.5 * f * f;
+  double dk = (double)k;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+/* FreeBSD msun e_logf.c */
+float or_log_f(float x) {
+  const float ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f;
+  const float Lg1 = 0.66666662693f, Lg2 = 0.40000972152f, Lg3 = 0.28498786688f, Lg4 = 0.24279078841f;
+  if (x != x) return x;
+  if (x < 0.0f) return from_bits_f(0x7fc00000u);
+  if (x == 0.0f) return -from_bits_f(0x7f800000u);
+  uint32_t u = bits_f(x);
+  if ((u >> 23) >= 0xff) return x;
+  int k = 0;
+  if ((u >> 23) == 0) { x = x * 33554432.0f; u = bits_f(x); k = -25; }
+  k += (int)(u >> 23) - 127;
+  float m = from_bits_f((u & 0x007fffffu) | 0x3f800000u);
+  if (m > 1.41421353816986083984f) { m = m * 0.5f; k += 1; }
+  float f = m - 1.0f;
+  float s = f / (2.0f + f);
+  float z = s * s, w = z * z;
+  float t1 = w * (Lg2 + w * Lg4);
+  float t2 = z * (Lg1 + w * Lg3);
+  float R = t2 + t1;
+  float hfsq = 0.5f * f * f;
+  float dk = (float)k;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+/* exp: FreeBSD msun e_exp.c, with k = (int)(x/ln2 +- 1/2) for every x */
+static double scale2_d(double y, int k) {
+  if (k > 1023) return y * from_bits_d(0x7fe0000000000000ull) * from_bits_d((uint64_t)(k) << 52);
+  if (k < -1021)
+    return y * from_bits_d((uint64_t)(k + 1000 + 1023) << 52) * from_bits_d((uint64_t)(23) << 52);
+  return y * from_bits_d((uint64_t)(k + 1023) << 52);
+}
+double or_exp_d(double x) {
+  const double o_th = 7.09782712893383973096e+02, u_th = -7.45133219101941108420e+02;
+  const double ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10;
+  const double invln2 = 1.44269504088896338700e+00;
+  const double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+               P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+               P5 = 4.13813679705723846039e-08;
+  if (x != x) return x;
+  if (x > o_th) return from_bits_d(0x7ff0000000000000ull);
+  if (x < u_th) return 0.0;
+  int k = (int)(invln2 * x + (x < 0.0 ? -0.5 : 0.5));
+  double dk = (double)k;
+  double hi = x - dk * ln2HI, lo = dk * ln2LO;
+  double r = hi - lo;
+  double t = r * r;
+  double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
+  double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
+  return scale2_d(y, k);
+}
+static float scale2_f(float y, int k) {
+  if (k > 127) return y * from_bits_f(0x7f000000u) * from_bits_f((uint32_t)(k) << 23);
+  if (k < -125) return y * from_bits_f((uint32_t)(k + 100 + 127) << 23) * from_bits_f((uint32_t)(27) << 23);
+  return y * from_bits_f((uint32_t)(k + 127) << 23);
+}
+float or_exp_f(float x) {
+  const float o_th = 8.8721679688e+01f, u_th = -1.0397208405e+02f;
+  const float ln2HI = 6.9314575195e-01f, ln2LO = 1.4286067653e-06f, invln2 = 1.4426950216e+00f;
+  const float P1 = 1.6666625440e-1f, P2 = -2.7667332906e-3f;
+  if (x != x) return x;
+  if (x > o_th) return from_bits_f(0x7f800000u);
+  if (x < u_th) return 0.0f;
+  int k = (int)(invln2 * x + (x < 0.0f ? -0.5f : 0.5f));
+  float dk = (float)k;
+  float hi = x - dk * ln2HI, lo = dk * ln2LO;
+  float r = hi - lo;
+  float t = r * r;
+  float c = r - t * (P1 + t * P2);
+  float y = 1.0f - ((lo - (r * c) / (2.0f - c)) - hi);
+  return scale2_f(y, k);
+}
+
+/* cos(2 pi u) for u in [0,1): symmetric reduction in u, fdlibm kernels (f64),
+ * Taylor kernels (f32). */
+static double ksin_d(double x) {
+  const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+               S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+               S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  double z = x * x, v = z * x;
+  double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+  return x + v * (S1 + z * r);
+}
+static double kcos_d(double x) {
+  const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+               C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+               C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+  double z = x * x, w = z * z;
+  double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+  double hz = 0.5 * z;
+  double ww = 1.0 - hz;
+  return ww + (((1.0 - ww) - hz) + z * r);
+}
+static float ksin_f(float x) {
+  float z = x * x;
+  return x + x * z * (-1.6666667163e-01f + z * (8.3333337680e-03f + z * (-1.9841270114e-04f + z * 2.7557314297e-06f)));
+}
+static float kcos_f(float x) {
+  float z = x * x;
+  return 1.0f - 0.5f * z + z * z * (4.1666667908e-02f + z * (-1.3888889225e-03f + z * (2.4801587642e-05f + z * -2.7557314297e-07f)));
+}
+double or_cos2pi_d(double u) {
+  const double twopi = 6.283185307179586476925286766559;
+  double a = u;
+  if (a > 0.5) a = 1.0 - a;
+  double sign = 1.0;
+  if (a > 0.25) { a = 0.5 - a; sign = -1.0; }
+  double r = (a <= 0.125) ? kcos_d(a * twopi) : ksin_d((0.25 - a) * twopi);
+  return sign * r;
+}
+float or_cos2pi_f(float u) {
+  const float twopi = (float)6.283185307179586476925286766559;
+  float a = u;
+  if (a > 0.5f) a = 1.0f - a;
+  float sign = 1.0f;
+  if (a > 0.25f) { a = 0.5f - a; sign = -1.0f; }
+  float r = (a <= 0.125f) ? kcos_f(a * twopi) : ksin_f((0.25f - a) * twopi);
+  return sign * r;
+}
+
+double or_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  uint32_t x[4];
+  draw(seed, chain, step, tag, idx, x);
+  double u1 = unif_oc_d(x[0], x[1]);
+  double u2 = unif_co_d(x[2], x[3]);
+  double r = sqrt(-2.0 * or_log_d(u1));
+  return r * or_cos2pi_d(u2);
+}
+float or_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  uint32_t x[4];
+  draw(seed, chain, step, tag, idx, x);
+  float u1 = unif_oc_f(x[0]);
+  float u2 = unif_co_f(x[2]);
+  float r = sqrtf(-2.0f * or_log_f(u1));
+  return r * or_cos2pi_f(u2);
+}
+double or_uniform_co_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  uint32_t x[4];
+  draw(seed, chain, step, tag, idx, x);
+  return unif_co_d(x[0], x[1]);
+}
+float or_uniform_co_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  uint32_t x[4];
+  draw(seed, chain, step, tag, idx, x);
+  return unif_co_f(x[0]);
+}
+static double uniform_oc_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  uint32_t x[4];
+  draw(seed, chain, step, tag, idx, x);
+  return unif_oc_d(x[0], x[1]);
+}
+static float uniform_oc_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  uint32_t x[4];
+  draw(seed, chain, step, tag, idx, x);
+  return unif_oc_f(x[0]);
+}
+
+/* ===================== threading helper ===================== */
+typedef struct {
+  void (*fn)(void* ctx, int64_t c0, int64_t c1);
+  void* ctx;
+  int64_t c0, c1;
+} or_job;
+static void* or_job_main(void* p) {
+  or_job* j = (or_job*)p;
+  j->fn(j->ctx, j->c0, j->c1);
+  return NULL;
+}
+static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, int64_t), void* ctx) {
+  if (threads <= 1 || C < 2) {
+    fn(ctx, 0, C);
+    return;
+  }
+  if (threads > C) threads = (int)C;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+  or_job* jobs = (or_job*)malloc(sizeof(or_job) * threads);
+  for (int i = 0; i < threads; ++i) {
+    jobs[i].fn = fn;
+    jobs[i].ctx = ctx;
+    jobs[i].c0 = C * i / threads;
+    jobs[i].c1 = C * (i + 1) / threads;
+    pthread_create(&th[i], NULL, or_job_main, &jobs[i]);
+  }
+  for (int i = 0; i < threads; ++i) pthread_join(th[i], NULL);
+  free(th);
+  free(jobs);
+}
+
+/* ===================== Part 2: templated samplers ===================== */
+#define CAT_(a, b) a##b
+#define CAT(a, b) CAT_(a, b)
+
+#define T double
+#define SFX _d
+#define LOG or_log_d
+#define EXP or_exp_d
+#define SQRT sqrt
+#define NORMAL or_normal_d
+#define UNIF_CO or_uniform_co_d
+#define UNIF_OC uniform_oc_d
+#define MACH_EPS 2.220446049250313e-16
+#include "gm_oracle_t.inc"
+#undef T
+#undef SFX
+#undef LOG
+#undef EXP
+#undef SQRT
+#undef NORMAL
+#undef UNIF_CO
+#undef UNIF_OC
+#undef MACH_EPS
+
+#define T float
+#define SFX _f
+#define LOG or_log_f
+#define EXP or_exp_f
+#define SQRT sqrtf
+#define NORMAL or_normal_f
+#define UNIF_CO or_uniform_co_f
+#define UNIF_OC uniform_oc_f
+#define MACH_EPS 1.1920928955078125e-07f
+#include "gm_oracle_t.inc"
+#undef T
+#undef SFX
+
+/* ===================== Part 3: diagnostics (stats.rs, f32) ===================== */
+
+/* ndarray-style contiguous f32 sum: eight interleaved accumulators, folded. */
+static float sum_f32(const float* v, int64_t n, int64_t stride) {
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int64_t i = 0;
+  for (; i + 8 <= n; i += 8)
+    for (int k = 0; k < 8; ++k) acc[k] += v[(i + k) * stride];
+  float tail = 0.0f;
+  for (; i < n; ++i) tail += v[i * stride];
+  return ((acc[0] + acc[4]) + (acc[1] + acc[5])) + ((acc[2] + acc[6]) + (acc[3] + acc[7])) + tail;
+}
+
+/* autocov_bf (stats.rs:659-681): x is [n][d] row-major */
+void or_autocov_bf(const float* x, int64_t n, int64_t d, float* out) {
+  float* col = (float*)malloc(sizeof(float) * (n > 0 ? n : 1));
+  for (int64_t c = 0; c < d; ++c) {
+    for (int64_t t = 0; t < n; ++t) col[t] = x[t * d + c];
+    float mean = sum_f32(col, n, 1) / (float)n;
+    for (int64_t t = 0; t < n; ++t) col[t] = col[t] - mean;
+    for (int64_t lag = 0; lag < n; ++lag) {
+      float s = 0.0f;
+      for (int64_t t = 0; t < n - lag; ++t) s += col[t] * col[t + lag];
+      out[lag * d + c] = s / (float)n;
+    }
+  }
+  free(col);
+}
+
+/* autocov_fft (stats.rs:603-647): zero-pad to a power of two >= 2n-1, FFT,
+ * |X|^2, inverse FFT, scale by 1/n_padded/n. Iterative radix-2 in f32. */
+static void fft_f32(float* re, float* im, int64_t n, int inverse) {
+  for (int64_t i = 1, j = 0; i < n; ++i) {
+    int64_t bit = n >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) {
+      float t = re[i]; re[i] = re[j]; re[j] = t;
+      t = im[i]; im[i] = im[j]; im[j] = t;
+    }
+  }
+  for (int64_t len = 2; len <= n; len <<= 1) {
+    double ang = 2.0 * 3.14159265358979323846 / (double)len * (inverse ? 1.0 : -1.0);
+    for (int64_t i = 0; i < n; i += len)
+      for (int64_t k = 0; k < len / 2; ++k) {
+        float wr = (float)cos(ang * (double)k), wi = (float)sin(ang * (double)k);
+        float ur = re[i + k], ui = im[i + k];
+        float vr = re[i + k + len / 2] * wr - im[i + k + len / 2] * wi;
+        float vi = re[i + k + len / 2] * wi + im[i + k + len / 2] * wr;
+        re[i + k] = ur + vr; im[i + k] = ui + vi;
+        re[i + k + len / 2] = ur - vr; im[i + k + len / 2] = ui - vi;
+      }
+  }
+}
+void or_autocov_fft(const float* x, int64_t n, int64_t d, float* out) {
+  int64_t np = 1;
+  while (np < 2 * n - 1) np <<= 1;
+  float* re = (float*)malloc(sizeof(float) * np);
+  float* im = (float*)malloc(sizeof(float) * np);
+  for (int64_t c = 0; c < d; ++c) {
+    float s = 0.0f;
+    for (int64_t t = 0; t < n; ++t) s += x[t * d + c];
+    float mean = s / (float)n;
+    for (int64_t t = 0; t < np; ++t) {
+      re[t] = t < n ? x[t * d + c] - mean : 0.0f;
+      im[t] = 0.0f;
+    }
+    fft_f32(re, im, np, 0);
+    for (int64_t t = 0; t < np; ++t) {
+      re[t] = re[t] * re[t] + im[t] * im[t];
+      im[t] = 0.0f;
+    }
+    fft_f32(re, im, np, 1);
+    for (int64_t t = 0; t < n; ++t) out[t * d + c] = re[t] / (float)np / (float)n;
+  }
+  free(re);
+  free(im);
+}
+
+/* split_rhat_mean_ess (stats.rs:439-573) on an f32 [C][N][P] sample. */
+void or_split_rhat_ess(const float* x, int64_t C, int64_t N, int64_t P, float* rhat, float* ess) {
+  const int64_t h = N / 2, K = 2 * C;
+  /* splitcat: [2C][h][P] */
+  float* y = (float*)malloc(sizeof(float) * (size_t)(K * h * P > 0 ? K * h * P : 1));
+  for (int64_t c = 0; c < C; ++c)
+    for (int64_t t = 0; t < h; ++t)
+      for (int64_t p = 0; p < P; ++p) {
+        y[(c * h + t) * P + p] = x[(c * N + t) * P + p];
+        y[((C + c) * h + t) * P + p] = x[(c * N + (N - h) + t) * P + p];
+      }
+  float* within = (float*)malloc(sizeof(float) * P);
+  float* var = (float*)malloc(sizeof(float) * P);
+  float* cms = (float*)malloc(sizeof(float) * K);
+  float* sq = (float*)malloc(sizeof(float) * K);
+  for (int64_t p = 0; p < P; ++p) { /* withinvar (stats.rs:456-504) */
+    for (int64_t k = 0; k < K; ++k) cms[k] = sum_f32(&y[(k * h) * P + p], h, P) / (float)h;
+    float overall = sum_f32(cms, K, 1) / (float)K;
+    for (int64_t k = 0; k < K; ++k) { float d = cms[k] - overall; sq[k] = d * d; }
+    float b = sum_f32(sq, K, 1) * ((float)h / (float)(K - 1));
+    for (int64_t k = 0; k < K; ++k) {
+      float s = 0.0f;
+      for (int64_t t = 0; t < h; ++t) {
+        float v = y[(k * h + t) * P + p];
+        s += (v - cms[k]) * (v - cms[k]);
+      }
+      sq[k] = s / (float)h;
+    }
+    float w = sum_f32(sq, K, 1) / (float)K;
+    within[p] = w;
+    var[p] = (((float)h - 1.0f) / (float)h) * w + b / (float)h;
+    rhat[p] = sqrtf(w / var[p]); /* rhat (stats.rs:452-454) */
+  }
+  /* ess (stats.rs:523-573): mean over chains of autocov, rho, Geyer */
+  float* avg = (float*)calloc((size_t)(h * P > 0 ? h * P : 1), sizeof(float));
+  float* ac = (float*)malloc(sizeof(float) * (size_t)(h * P > 0 ? h * P : 1));
+  for (int64_t k = 0; k < K; ++k) {
+    if (h <= 100) or_autocov_bf(&y[k * h * P], h, P, ac);
+    else or_autocov_fft(&y[k * h * P], h, P, ac);
+    for (int64_t i = 0; i < h * P; ++i) avg[i] += ac[i];
+  }
+  for (int64_t i = 0; i < h * P; ++i) avg[i] = avg[i] / (float)K;
+  for (int64_t p = 0; p < P; ++p) {
+    float mn = (h >= 2) ? (1.0f - (within[p] - avg[0 * P + p]) / var[p]) +
+                              (1.0f - (within[p] - avg[1 * P + p]) / var[p])
+                        : 0.0f;
+    float out = 0.0f;
+    for (int64_t i = 0; 2 * i + 1 < h; ++i) {
+      float r0 = 1.0f - (within[p] - avg[(2 * i) * P + p]) / var[p];
+      float r1 = 1.0f - (within[p] - avg[(2 * i + 1) * P + p]) / var[p];
+      float pt = r0 + r1;
+      if (pt <= 0.0f) break;
+      if (pt > mn) pt = mn;
+      mn = pt;
+      out += pt;
+    }
+    float tau = -1.0f + 2.0f * out;
+    ess[p] = (1.0f / tau) * (float)K * (float)h;
+  }
+  free(y); free(within); free(var); free(cms); free(sq); free(avg); free(ac);
+}
+
+/* MultiChainTracker (stats.rs:199-339): step() updates, then rhat(). */
+void or_mct_rhat(const float* steps, int64_t nsteps, int64_t C, int64_t P, float* rhat) {
+  float* mean = (float*)calloc((size_t)(C * P), sizeof(float));
+  float* mean_sq = (float*)calloc((size_t)(C * P), sizeof(float));
+  for (int64_t s = 0; s < nsteps; ++s) {
+    float n = (float)(s + 1);
+    for (int64_t i = 0; i < C * P; ++i) {
+      float x = steps[s * C * P + i];
+      mean[i] = (mean[i] * (n - 1.0f) + x) / n;
+      if (s == 0) mean_sq[i] = x * x;
+      else mean_sq[i] = (mean_sq[i] * (n - 1.0f) + x * x) / n;
+    }
+  }
+  float n = (float)nsteps, nc = (float)C;
+  float fac = n / (nc - 1.0f);
+  for (int64_t p = 0; p < P; ++p) {
+    float mc = 0.0f;
+    for (int64_t c = 0; c < C; ++c) mc += mean[c * P + p];
+    mc /= nc;
+    float between = 0.0f, within = 0.0f;
+    for (int64_t c = 0; c < C; ++c) {
+      float d = mean[c * P + p] - mc;
+      between += d * d;
+    }
+    between *= fac;
+    for (int64_t c = 0; c < C; ++c) {
+      float m = mean[c * P + p];
+      within += (mean_sq[c * P + p] - m * m) * n / (n - 1.0f);
+    }
+    within /= nc;
+    float v = within * ((n - 1.0f) / n) + between * (1.0f / n);
+    rhat[p] = sqrtf(v / within);
+  }
+  free(mean);
+  free(mean_sq);
+}
+
+/* ===================== KAT entry points (double) ===================== */
+double or_find_reasonable_epsilon_d(const or_target* t, int lanes, int elems, const double* q,
+                                    const double* p) {
+  nctx_d cx;
+  memset(&cx, 0, sizeof(cx));
+  cx.t = t; cx.lanes = lanes; cx.elems = elems; cx.D = t->dim;
+  cx.tmpv = (double*)malloc(sizeof(double) * t->dim);
+  double e = find_eps_d(&cx, q, p);
+  free(cx.tmpv);
+  return e;
+}
+
+void or_build_tree_d(const or_target* t, int lanes, int elems, const double* q, const double* p,
+                     const double* g, double logu, int v, int j, double eps, double joint0,
+                     uint64_t seed, uint32_t chain, uint64_t step, double* out_vecs,
+                     double* out_scalars) {
+  const int D = t->dim;
+  nctx_d cx;
+  memset(&cx, 0, sizeof(cx));
+  cx.t = t; cx.lanes = lanes; cx.elems = elems; cx.D = D;
+  cx.seed = seed; cx.cid = chain; cx.step = step;
+  for (int k = 0; k < 32; ++k) tree_alloc_d(&cx.ws[k], D);
+  cx.tmpv = (double*)malloc(sizeof(double) * D);
+  tree_d out;
+  tree_alloc_d(&out, D);
+  build_tree_d(&cx, q, p, g, logu, v, j, eps, joint0, &out);
+  const double* vs[8] = {out.qm, out.pm, out.gm, out.qp, out.pp, out.gp, out.qprime, out.gprime};
+  for (int k = 0; k < 8; ++k) memcpy(out_vecs + k * D, vs[k], sizeof(double) * D);
+  out_scalars[0] = out.logp_prime;
+  out_scalars[1] = (double)out.n;
+  out_scalars[2] = (double)out.s;
+  out_scalars[3] = out.alpha;
+  out_scalars[4] = (double)out.n_alpha;
+  for (int k = 0; k < 32; ++k) free(cx.ws[k].qm);
+  free(out.qm);
+  free(cx.tmpv);
+}

@@ -1,0 +1,110 @@
+/*
+ * gm_oracle.h — CPU ORACLE (test infrastructure only; never linked into the
+ * product). A plain-C restatement of the reference algorithms of
+ * SauersML/general-mcmc for the HMC / NUTS / MH / split-R-hat path, driven by
+ * the engine's documented random-number spec so that the GPU kernels can be
+ * checked bit-for-bit on the same inputs.
+ *
+ * Parity pins: the reference's RNG-free known-answer tests (tests/golden/
+ * reference_kat.json, see tests/test_oracle_kat.py): build_tree
+ * (nuts.rs:521-586), find_reasonable_epsilon (nuts.rs:508-519), chain_1
+ * (nuts.rs:588-601), MultiChainTracker R-hat (stats.rs:734-783), autocov BF
+ * and FFT (stats.rs:808-839), IsotropicGaussian / Gaussian2D densities
+ * (distributions.rs:580-614, 820-839) and the mass-matrix algebra
+ * (generic_nuts.rs:1427-1489). The reference's random streams (rand 0.9
+ * SmallRng, rand_distr, burn backend RNG) cannot be reproduced offline; sample
+ * streams are therefore pinned to the engine's Philox spec, not to the
+ * reference's bits.
+ *
+ * Summation order: per-chain sums (kinetic energy, log-density, U-turn dots)
+ * are taken in the engine's declared order, parameterised by the lane layout
+ * (lanes x elems): each lane sums its elems left to right, then an xor
+ * butterfly over lanes (offsets 1, 2, 4, ...).
+ */
+#ifndef GM_ORACLE_H
+#define GM_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_target {
+  int32_t kind; /* 1 rosenbrock, 2 iso gauss, 3 gauss */
+  int32_t dim;
+  double a, b, std;
+  const double* mean; /* [dim] */
+  const double* prec; /* [dim*dim] */
+  double norm_const;
+} or_target;
+
+/* ---- RNG spec ---- */
+void or_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+double or_log_d(double x);
+float or_log_f(float x);
+double or_exp_d(double x);
+float or_exp_f(float x);
+double or_cos2pi_d(double u);
+float or_cos2pi_f(float u);
+double or_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
+float or_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
+double or_uniform_co_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
+float or_uniform_co_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
+
+/* ---- targets ---- */
+double or_logp_grad_d(const or_target* t, int lanes, int elems, const double* x, double* g);
+float or_logp_grad_f(const or_target* t, int lanes, int elems, const float* x, float* g);
+
+/* ---- HMC: batched_hmc.rs:129-190 per chain ---- */
+int or_hmc_run_d(const or_target* t, int lanes, int elems, int64_t C, int D, double* q, double eps,
+                 int L, uint64_t seed, uint64_t step0, uint32_t chain_offset, int64_t n_steps,
+                 int64_t collect_from, double* samples, int64_t* accepts, int threads);
+int or_hmc_run_f(const or_target* t, int lanes, int elems, int64_t C, int D, float* q, double eps,
+                 int L, uint64_t seed, uint64_t step0, uint32_t chain_offset, int64_t n_steps,
+                 int64_t collect_from, float* samples, int64_t* accepts, int threads);
+
+/* ---- MH: metropolis_hastings.rs:306-318 per chain ---- */
+int or_mh_run_d(const or_target* t, int lanes, int elems, int64_t C, int D, double* q,
+                double prop_std, uint64_t seed, uint64_t step0, uint32_t chain_offset,
+                int64_t n_steps, int64_t collect_from, double* samples, int64_t* accepts,
+                int threads);
+int or_mh_run_f(const or_target* t, int lanes, int elems, int64_t C, int D, float* q,
+                double prop_std, uint64_t seed, uint64_t step0, uint32_t chain_offset,
+                int64_t n_steps, int64_t collect_from, float* samples, int64_t* accepts,
+                int threads);
+
+/* ---- NUTS: generic_nuts.rs:731-1418 per chain (identity mass) ----
+ * state arrays eps/eps_bar/h_bar/mu are [C]; progress selects run_progress
+ * semantics; samples [n_collect][C][D]. init_step is the counter value of the
+ * init draw; transitions use init_step + 0 .. total-1. */
+int or_nuts_run_d(const or_target* t, int lanes, int elems, int64_t C, int D, double* q,
+                  double* eps, double* eps_bar, double* h_bar, double* mu, double target_accept,
+                  int max_depth, uint64_t seed, uint64_t init_step, uint32_t chain_offset,
+                  int64_t n_collect, int64_t n_discard, int progress, double* samples,
+                  int64_t* accepts, int64_t* n_leapfrog, int threads);
+int or_nuts_run_f(const or_target* t, int lanes, int elems, int64_t C, int D, float* q,
+                  float* eps, float* eps_bar, float* h_bar, float* mu, double target_accept,
+                  int max_depth, uint64_t seed, uint64_t init_step, uint32_t chain_offset,
+                  int64_t n_collect, int64_t n_discard, int progress, float* samples,
+                  int64_t* accepts, int64_t* n_leapfrog, int threads);
+double or_find_reasonable_epsilon_d(const or_target* t, int lanes, int elems, const double* q,
+                                    const double* p);
+/* build_tree (generic_nuts.rs:1105-1341), identity mass; out vectors [dim]:
+ * qm pm gm qp pp gp qprime gprime; scalars logp_prime, n, s, alpha, n_alpha.
+ * merge uniforms come from (seed, chain, step, MRG, counter). */
+void or_build_tree_d(const or_target* t, int lanes, int elems, const double* q, const double* p,
+                     const double* g, double logu, int v, int j, double eps, double joint0,
+                     uint64_t seed, uint32_t chain, uint64_t step, double* out_vecs,
+                     double* out_scalars);
+
+/* ---- diagnostics: stats.rs (f32, the reference's arithmetic) ---- */
+void or_split_rhat_ess(const float* x, int64_t C, int64_t N, int64_t P, float* rhat, float* ess);
+void or_autocov_bf(const float* x, int64_t n, int64_t d, float* out);
+void or_autocov_fft(const float* x, int64_t n, int64_t d, float* out);
+/* MultiChainTracker: steps [nsteps][C][P] -> rhat [P] (stats.rs:199-339) */
+void or_mct_rhat(const float* steps, int64_t nsteps, int64_t C, int64_t P, float* rhat);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,223 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle.so) -- test
+infrastructure only: the checker the GPU results are compared with."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+
+_vp, _i64, _i32, _u64, _u32, _dbl, _flt, _int = (C.c_void_p, C.c_int64, C.c_int32, C.c_uint64,
+                                                   C.c_uint32, C.c_double, C.c_float, C.c_int)
+
+
+class or_target(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("dim", C.c_int32), ("a", C.c_double), ("b", C.c_double),
+                ("std", C.c_double), ("mean", C.POINTER(C.c_double)),
+                ("prec", C.POINTER(C.c_double)), ("norm_const", C.c_double)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return Oracle(_lib)
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
+            os.path.getmtime(os.path.join(ORACLE_DIR, f))
+            for f in ("gm_oracle.c", "gm_oracle_t.inc", "gm_oracle.h")):
+        build()
+    lib = C.CDLL(LIB)
+    tp = C.POINTER(or_target)
+    for sfx, rt in (("d", _dbl), ("f", _flt)):
+        getattr(lib, f"or_log_{sfx}").restype = rt
+        getattr(lib, f"or_log_{sfx}").argtypes = [rt]
+        getattr(lib, f"or_exp_{sfx}").restype = rt
+        getattr(lib, f"or_exp_{sfx}").argtypes = [rt]
+        getattr(lib, f"or_cos2pi_{sfx}").restype = rt
+        getattr(lib, f"or_cos2pi_{sfx}").argtypes = [rt]
+        getattr(lib, f"or_normal_{sfx}").restype = rt
+        getattr(lib, f"or_normal_{sfx}").argtypes = [_u64, _u32, _u64, _u32, _u32]
+        getattr(lib, f"or_uniform_co_{sfx}").restype = rt
+        getattr(lib, f"or_uniform_co_{sfx}").argtypes = [_u64, _u32, _u64, _u32, _u32]
+        getattr(lib, f"or_logp_grad_{sfx}").restype = rt
+        getattr(lib, f"or_logp_grad_{sfx}").argtypes = [tp, _int, _int, _vp, _vp]
+        getattr(lib, f"or_hmc_run_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _dbl, _int,
+                                                      _u64, _u64, _u32, _i64, _i64, _vp, _vp, _int]
+        getattr(lib, f"or_mh_run_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _dbl, _u64,
+                                                     _u64, _u32, _i64, _i64, _vp, _vp, _int]
+        getattr(lib, f"or_nuts_run_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _vp, _vp,
+                                                       _vp, _vp, _dbl, _int, _u64, _u64, _u32,
+                                                       _i64, _i64, _int, _vp, _vp, _vp, _int]
+    lib.or_philox.argtypes = [C.POINTER(C.c_uint32)] * 3
+    lib.or_find_reasonable_epsilon_d.restype = _dbl
+    lib.or_find_reasonable_epsilon_d.argtypes = [tp, _int, _int, _vp, _vp]
+    lib.or_build_tree_d.argtypes = [tp, _int, _int, _vp, _vp, _vp, _dbl, _int, _int, _dbl, _dbl,
+                                    _u64, _u32, _u64, _vp, _vp]
+    lib.or_split_rhat_ess.argtypes = [_vp, _i64, _i64, _i64, _vp, _vp]
+    lib.or_autocov_bf.argtypes = [_vp, _i64, _i64, _vp]
+    lib.or_autocov_fft.argtypes = [_vp, _i64, _i64, _vp]
+    lib.or_mct_rhat.argtypes = [_vp, _i64, _i64, _i64, _vp]
+    _lib = lib
+    return Oracle(lib)
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _sfx(dtype):
+    return "d" if np.dtype(dtype) == np.float64 else "f"
+
+
+class Target:
+    """Oracle-side description of a built-in target (mirrors gm_target)."""
+
+    def __init__(self, kind, dim, a=1.0, b=100.0, std=1.0, mean=None, prec=None, norm_const=0.0):
+        self.kind, self.dim, self.a, self.b, self.std = kind, dim, a, b, std
+        self.mean = None if mean is None else np.ascontiguousarray(mean, dtype=np.float64)
+        self.prec = None if prec is None else np.ascontiguousarray(prec, dtype=np.float64)
+        self.norm_const = norm_const
+
+    @classmethod
+    def from_product(cls, t, dim):
+        """Same parameters as a general_mcmc_amd target."""
+        st, _ = t.to_struct(dim)
+        mean = prec = None
+        if st.kind == 3:
+            mean = np.asarray(t.mean, dtype=np.float64)
+            prec = np.asarray(t.inv_cov, dtype=np.float64)
+        return cls(st.kind, dim, st.a, st.b, st.std, mean, prec, st.norm_const)
+
+    def struct(self):
+        t = or_target()
+        t.kind, t.dim, t.a, t.b, t.std, t.norm_const = (self.kind, self.dim, self.a, self.b,
+                                                         self.std, self.norm_const)
+        if self.mean is not None:
+            t.mean = self.mean.ctypes.data_as(C.POINTER(C.c_double))
+            t.prec = self.prec.ctypes.data_as(C.POINTER(C.c_double))
+        return t
+
+
+class Oracle:
+    def __init__(self, lib):
+        self.lib = lib
+
+    def philox(self, ctr, key):
+        a = (C.c_uint32 * 4)(*ctr)
+        k = (C.c_uint32 * 2)(*key)
+        o = (C.c_uint32 * 4)()
+        self.lib.or_philox(a, k, o)
+        return list(o)
+
+    def logp_grad(self, target: Target, x, lanes, elems, dtype):
+        x = np.ascontiguousarray(np.atleast_2d(x), dtype=dtype)
+        n, d = x.shape
+        lp = np.empty(n, dtype=dtype)
+        g = np.zeros((n, lanes * elems), dtype=dtype)
+        t = target.struct()
+        fn = getattr(self.lib, f"or_logp_grad_{_sfx(dtype)}")
+        for i in range(n):
+            lp[i] = fn(C.byref(t), lanes, elems, _p(x[i]), g[i].ctypes.data_as(C.c_void_p))
+        return lp, np.ascontiguousarray(g[:, :d])
+
+    def hmc_run(self, target: Target, q, eps, L, seed, step0, n_steps, collect_from, lanes, elems,
+                chain_offset=0, threads=8):
+        q = np.array(q, copy=True, order="C")
+        C_, D = q.shape
+        rows = max(0, n_steps - collect_from)
+        samples = np.zeros((rows, C_, D), dtype=q.dtype)
+        acc = np.zeros(C_, dtype=np.int64)
+        t = target.struct()
+        rc = getattr(self.lib, f"or_hmc_run_{_sfx(q.dtype)}")(
+            C.byref(t), lanes, elems, C_, D, _p(q), eps, L, seed, step0, chain_offset, n_steps,
+            collect_from, _p(samples), _p(acc), threads)
+        assert rc == 0
+        return q, samples, acc
+
+    def mh_run(self, target: Target, q, prop_std, seed, step0, n_steps, collect_from, lanes, elems,
+               chain_offset=0, threads=8):
+        q = np.array(q, copy=True, order="C")
+        C_, D = q.shape
+        rows = max(0, n_steps - collect_from)
+        samples = np.zeros((rows, C_, D), dtype=q.dtype)
+        acc = np.zeros(C_, dtype=np.int64)
+        t = target.struct()
+        rc = getattr(self.lib, f"or_mh_run_{_sfx(q.dtype)}")(
+            C.byref(t), lanes, elems, C_, D, _p(q), prop_std, seed, step0, chain_offset, n_steps,
+            collect_from, _p(samples), _p(acc), threads)
+        assert rc == 0
+        return q, samples, acc
+
+    def nuts_state(self, n, dtype):
+        return {"eps": np.full(n, -1.0, dtype=dtype), "eps_bar": np.ones(n, dtype=dtype),
+                "h_bar": np.zeros(n, dtype=dtype),
+                "mu": np.full(n, np.log(10.0), dtype=dtype)}
+
+    def nuts_run(self, target: Target, q, state, target_accept, max_depth, seed, init_step,
+                 n_collect, n_discard, progress, lanes, elems, chain_offset=0, threads=8):
+        q = np.array(q, copy=True, order="C")
+        C_, D = q.shape
+        samples = np.zeros((n_collect, C_, D), dtype=q.dtype)
+        acc = np.zeros(C_, dtype=np.int64)
+        nlf = np.zeros(C_, dtype=np.int64)
+        t = target.struct()
+        rc = getattr(self.lib, f"or_nuts_run_{_sfx(q.dtype)}")(
+            C.byref(t), lanes, elems, C_, D, _p(q), _p(state["eps"]), _p(state["eps_bar"]),
+            _p(state["h_bar"]), _p(state["mu"]), target_accept, max_depth, seed, init_step,
+            chain_offset, n_collect, n_discard, int(progress), _p(samples), _p(acc), _p(nlf),
+            threads)
+        assert rc == 0
+        return q, samples, acc, nlf
+
+    def split_rhat_ess(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        c, n, p = x.shape
+        r = np.empty(p, dtype=np.float32)
+        e = np.empty(p, dtype=np.float32)
+        self.lib.or_split_rhat_ess(_p(x), c, n, p, _p(r), _p(e))
+        return r, e
+
+    def autocov(self, x, fft=False):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        n, d = x.shape
+        out = np.empty((n, d), dtype=np.float32)
+        (self.lib.or_autocov_fft if fft else self.lib.or_autocov_bf)(_p(x), n, d, _p(out))
+        return out
+
+    def mct_rhat(self, steps):
+        s = np.ascontiguousarray(steps, dtype=np.float32)
+        ns, c, p = s.shape
+        r = np.empty(p, dtype=np.float32)
+        self.lib.or_mct_rhat(_p(s), ns, c, p, _p(r))
+        return r
+
+    def find_reasonable_epsilon(self, target: Target, q, p, lanes=64, elems=1):
+        t = target.struct()
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        p = np.ascontiguousarray(p, dtype=np.float64)
+        return self.lib.or_find_reasonable_epsilon_d(C.byref(t), lanes, elems, _p(q), _p(p))
+
+    def build_tree(self, target: Target, q, p, g, logu, v, j, eps, joint0, seed=0, chain=0, step=0,
+                   lanes=64, elems=1):
+        t = target.struct()
+        d = target.dim
+        vecs = np.zeros((8, d), dtype=np.float64)
+        sc = np.zeros(5, dtype=np.float64)
+        q, p, g = (np.ascontiguousarray(a, dtype=np.float64) for a in (q, p, g))
+        self.lib.or_build_tree_d(C.byref(t), lanes, elems, _p(q), _p(p), _p(g), logu, v, j, eps,
+                                 joint0, seed, chain, step, _p(vecs), _p(sc))
+        names = ["qm", "pm", "gm", "qp", "pp", "gp", "qprime", "gprime"]
+        out = {k: vecs[i] for i, k in enumerate(names)}
+        out.update(logp_prime=sc[0], n=int(sc[1]), s=bool(sc[2]), alpha=sc[3], n_alpha=int(sc[4]))
+        return out

@@ -1,0 +1,60 @@
+"""The RNG spec the engine and the oracle share: Philox4x32-10 known answers
+(Random123 kat_vectors) and the special functions' accuracy. CPU only."""
+import math
+
+import numpy as np
+import pytest
+
+
+def test_philox_random123_kat(oracle):
+    assert oracle.philox([0, 0, 0, 0], [0, 0]) == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    assert oracle.philox([0xffffffff] * 4, [0xffffffff] * 2) == [
+        0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
+    assert oracle.philox([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344],
+                         [0xa4093822, 0x299f31d0]) == [0xd16cfe09, 0x94fdcceb, 0x5001e420,
+                                                       0x24126ea1]
+
+
+def _ulps(a, b, dt):
+    a = np.asarray(a, dtype=dt).astype(np.float64)
+    b = np.asarray(b, dtype=dt)
+    return np.max(np.abs(a - b.astype(np.float64)) / np.spacing(np.abs(b)).astype(np.float64))
+
+
+def test_log_exp_within_one_ulp(oracle):
+    rng = np.random.default_rng(0)
+    x = rng.uniform(1e-300, 1, 4000)
+    assert _ulps([oracle.lib.or_log_d(v) for v in x], np.log(x), np.float64) <= 1.0
+    xf = rng.uniform(1e-30, 1, 4000).astype(np.float32)
+    assert _ulps([oracle.lib.or_log_f(float(v)) for v in xf],
+                 np.log(xf.astype(np.float64)).astype(np.float32), np.float32) <= 1.0
+    y = rng.uniform(-700, 700, 4000)
+    assert _ulps([oracle.lib.or_exp_d(v) for v in y], np.exp(y), np.float64) <= 1.0
+    yf = rng.uniform(-80, 80, 4000).astype(np.float32)
+    assert _ulps([oracle.lib.or_exp_f(float(v)) for v in yf],
+                 np.exp(yf.astype(np.float64)).astype(np.float32), np.float32) <= 1.0
+    # edge cases
+    assert oracle.lib.or_log_d(0.0) == -math.inf
+    assert math.isnan(oracle.lib.or_log_d(-1.0))
+    assert oracle.lib.or_exp_d(1000.0) == math.inf
+    assert oracle.lib.or_exp_d(-1000.0) == 0.0
+    assert oracle.lib.or_log_d(5e-324) == pytest.approx(math.log(5e-324), rel=1e-15)
+
+
+def test_cos2pi_accuracy(oracle):
+    u = np.linspace(0, 1, 5001, endpoint=False)
+    assert np.max(np.abs(np.array([oracle.lib.or_cos2pi_d(v) for v in u]) - np.cos(2 * np.pi * u))) < 2e-15
+    uf = u.astype(np.float32)
+    err = np.abs(np.array([oracle.lib.or_cos2pi_f(float(v)) for v in uf]) -
+                 np.cos(2 * np.pi * uf.astype(np.float64)))
+    assert err.max() < 2.5e-7
+
+
+@pytest.mark.parametrize("sfx", ["d", "f"])
+def test_normal_stream_moments(oracle, sfx):
+    fn = getattr(oracle.lib, f"or_normal_{sfx}")
+    z = np.array([fn(7, c, 3, 2, d) for c in range(300) for d in range(100)])
+    assert abs(z.mean()) < 0.02
+    assert abs(z.std() - 1) < 0.02
+    assert abs(np.mean(z ** 3)) < 0.06
+    assert abs(np.mean(z ** 4) - 3) < 0.15
