@@ -7,37 +7,71 @@
 // stay exactly 0.
 //
 // Reduction order (the engine's defined summation order, mirrored by the CPU
-// oracle): each lane sums its E terms left to right, then an xor butterfly
-// over offsets 1,2,4,...,LPC/2. Addition is commutative in IEEE arithmetic, so
-// every lane of the group ends with the identical total.
+// oracle): each lane sums its E terms left to right, then pairwise stages over
+// the group's lanes, stage k combining lane l with lane partner_k(l):
+//   l^1, l^2 (DPP quad_perm), l^7 (DPP row_half_mirror), l^15 (DPP row_mirror),
+//   l^16, l^32 (ds_swizzle / bpermute),
+// as many stages as log2(LPC). Each partner map is an involution and IEEE
+// addition is commutative, so every lane of the group ends with the same total.
 #pragma once
 #include "gm_rng.h"
 
 namespace gm {
 
+// DPP move of a 32/64-bit value: lane l receives the value of the lane that
+// the DPP control selects (sources out of range read 0).
+template <int CTRL> __device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               0xf, 0xf, true));
+}
+template <int CTRL> __device__ __forceinline__ int dpp(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, true);
+}
+template <int CTRL> __device__ __forceinline__ double dpp(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xf, 0xf, true);
+  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+enum : int {
+  DPP_QUAD_XOR1 = 0xB1,   // quad_perm [1,0,3,2]
+  DPP_QUAD_XOR2 = 0x4E,   // quad_perm [2,3,0,1]
+  DPP_ROW_HALF_MIRROR = 0x141,
+  DPP_ROW_MIRROR = 0x140,
+  DPP_WAVE_SHL1 = 0x130,  // lane l <- lane l+1 (measured on gfx950, tools/probes/dpp_probe.hip)
+  DPP_WAVE_SHR1 = 0x138   // lane l <- lane l-1
+};
+
 template <int LPC, class T> __device__ __forceinline__ T group_sum(T v) {
-#pragma unroll
-  for (int off = 1; off < LPC; off <<= 1) v = v + __shfl_xor(v, off, LPC);
+  if constexpr (LPC >= 2) v = v + dpp<DPP_QUAD_XOR1>(v);
+  if constexpr (LPC >= 4) v = v + dpp<DPP_QUAD_XOR2>(v);
+  if constexpr (LPC >= 8) v = v + dpp<DPP_ROW_HALF_MIRROR>(v);
+  if constexpr (LPC >= 16) v = v + dpp<DPP_ROW_MIRROR>(v);
+  if constexpr (LPC >= 32) v = v + __shfl_xor(v, 16, 64);
+  if constexpr (LPC >= 64) v = v + __shfl_xor(v, 32, 64);
   return v;
 }
-// lane l of the group receives lane l+1's value (last lane: own value)
+// lane l receives lane l+1's value. Wave-wide DPP shift: at a group's last
+// lane the value comes from the next group (or 0); callers mask it, since a
+// group's last coordinate never has a successor inside the chain.
 template <int LPC, class T> __device__ __forceinline__ T from_next(T v) {
   if constexpr (LPC == 1) return v;
-  else return __shfl_down(v, 1, LPC);
+  else return dpp<DPP_WAVE_SHL1>(v);
 }
-// lane l of the group receives lane l-1's value (first lane: own value)
+// lane l receives lane l-1's value (group's first lane: masked by callers)
 template <int LPC, class T> __device__ __forceinline__ T from_prev(T v) {
   if constexpr (LPC == 1) return v;
-  else return __shfl_up(v, 1, LPC);
+  else return dpp<DPP_WAVE_SHR1>(v);
 }
 
 // ---------------------------------------------------------------------------
 // Rosenbrock: logp = -sum_{i<=D-2} [ b*(x_{i+1}-x_i^2)^2 + (a-x_i)^2 ]
 // RosenbrockND (distributions.rs:544-554) is a=1, b=100; Rosenbrock2D
 // (distributions.rs:502-515) is D=2 with free a,b. Gradient (analytic form of
-// what autodiff computes, hmc.rs:42-61):
-//   g_i = [i<=D-2] ( (4b x_i) t_i + 2 (a - x_i) ) - [i>=1] (2b t_{i-1}),
-//   t_i = x_{i+1} - x_i^2.
+// what autodiff computes, hmc.rs:42-61), evaluated branch-free as
+//   g_i = A_i - B_i,  A_i = [i<=D-2] ( (4b x_i) t_i + 2 (a - x_i) ),
+//                     B_i = [1<=i<=D-1] (2b t_{i-1}),   t_i = x_{i+1} - x_i^2
+// ([.] selects +0 when false).
 template <class T> struct RosenbrockT {
   T a, b, b2, b4;  // b2 = 2b, b4 = 4b (rounded once, host side)
   int D;
@@ -55,20 +89,15 @@ template <class T> struct RosenbrockT {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
+      const bool hs = i <= D - 2;
+      const bool hp = (i >= 1) & (i <= D - 1);
       const T tprev = (e > 0) ? t[(e > 0) ? e - 1 : 0] : tp;
       const T am = a - x[e];
-      T gi;
-      if (i <= D - 2) {
-        gi = (b4 * x[e]) * t[e] + (T)2 * am;
-        if (i >= 1) gi = gi - b2 * tprev;
-      } else if (i == D - 1 && i >= 1) {
-        gi = -(b2 * tprev);
-      } else {
-        gi = (T)0;
-      }
-      g[e] = gi;
+      const T A = hs ? (b4 * x[e]) * t[e] + (T)2 * am : (T)0;
+      const T B = hp ? b2 * tprev : (T)0;
+      g[e] = A - B;
       if (LOGP) {
-        const T s = (i <= D - 2) ? (b * (t[e] * t[e]) + am * am) : (T)0;
+        const T s = hs ? (b * (t[e] * t[e]) + am * am) : (T)0;
         part = (e == 0) ? s : part + s;
       }
     }

@@ -435,7 +435,8 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
   GM_HIP(hipSetDevice(s->device));
   s->last_ms = 0;
   s->last_launches = 0;
-  if (total <= 0) return GM_OK;
+  // NUTS always launches: init_chain_state + row 0 even with zero transitions
+  if (total <= 0 && s->kind != K_NUTS) return GM_OK;
   if (s->kind == K_NUTS) {
     int rc = nuts_run(s->nuts, s->dt, s->tg, s->lay, s->d_q, s->d_acc, s->d_samples, s->C, s->D,
                       s->target_accept, s->seed, &s->step, s->chain_offset, total, collect_from,
