@@ -7,10 +7,21 @@
 // metropolis_hastings.rs:313) and from burn's backend-global RNG
 // (euclidean.rs:484-509). Neither stream can be reproduced here (no crate
 // sources), and a serial stream cannot be split across 10^5 chains anyway.
-// Every random number in this engine is instead a pure function
-//     philox4x32_10(counter = {idx, chain, step, tag|step_hi}, key = seed)
+// Every random number in this engine is instead a pure function of
+//     (seed, chain, step, tag, idx)
 // so a chain's draws do not depend on how chains are placed on lanes, waves or
 // GPUs (bitwise-identical samples at 1/2/4/8 GPUs).
+//
+// Stream spec (v2). One Philox4x32-10 block
+//     x = philox(counter = {idx, chain, blk, tag | blk_hi << 8}, key = seed),
+//     blk = step / S,  S = 4 for f32 draws, 2 for f64 draws,
+// serves S consecutive steps: f32 uniforms use one word each (u_k from x_k,
+// k = step % 4); f64 uniforms use two words (u_k from x_{2k}, x_{2k+1},
+// k = step % 2). Normals come in Box-Muller pairs that use both branches:
+// f32 (z0,z1) from (u0,u1), (z2,z3) from (u2,u3); f64 (z0,z1) from (u0,u1),
+// with z_{2j} = r cos(2 pi u_{2j+1}), z_{2j+1} = r sin(2 pi u_{2j+1}),
+// r = sqrt(-2 ln u_{2j}) (u_{2j} from the (0,1] form); the draw for `step` is
+// z_{step % S}. A kernel that runs consecutive steps computes each block once.
 //
 // Bit-exactness rules (both sides): only IEEE +,-,*,/ and sqrt (correctly
 // rounded on gfx950 and x86), no FMA contraction (-ffp-contract=off), and our
@@ -64,10 +75,6 @@ GM_HD u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
   return c;
 }
 
-GM_HD u32x4 draw(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
-  u32x4 c{idx, chain, (uint32_t)step, tag | ((uint32_t)(step >> 32) << 8)};
-  return philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-}
 
 // ---- bit casts -------------------------------------------------------------
 GM_HD uint32_t f2u(float f) {
@@ -232,7 +239,9 @@ GM_HD float gexp(float x) {
   return scale2f(y, k);
 }
 
-// ---- cos(2*pi*u), u in [0,1) -------------------------------------------------
+// ---- cos / sin of 2*pi*u, u in [0,1) ---------------------------------------
+// Quadrant q = floor(4u), r = u - q/4 in [0, 1/4) (both exact); the first
+// octant uses the sine/cosine kernels directly, the second their complements.
 GM_HD double ksin(double x) {
   const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
                S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
@@ -259,38 +268,125 @@ GM_HD float kcos(float x) {
   const float z = x * x;
   return 1.0f - 0.5f * z + z * z * (4.1666667908e-02f + z * (-1.3888889225e-03f + z * (2.4801587642e-05f + z * -2.7557314297e-07f)));
 }
-template <class T> GM_HD T cos2pi(T u) {
+template <class T> GM_HD void sincos2pi(T u, T* c, T* s) {
   const T twopi = (T)6.283185307179586476925286766559;
-  T a = u;                          // u in [0,1)
-  if (a > (T)0.5) a = (T)1.0 - a;   // cos(2pi u) = cos(2pi (1-u)); 1-u exact for u in (0.5,1)
-  T sign = (T)1.0;
-  if (a > (T)0.25) { a = (T)0.5 - a; sign = (T)-1.0; }  // cos(pi - x) = -cos x
-  T r;
-  if (a <= (T)0.125) r = kcos(a * twopi);
-  else r = ksin(((T)0.25 - a) * twopi);               // cos(pi/2 - y) = sin y
-  return sign * r;
+  const T f4 = u * (T)4;
+  const int q = (int)f4;          // u in [0,1): q in 0..3
+  const T r = u - (T)q * (T)0.25;  // exact
+  T c0, s0;
+  if (r <= (T)0.125) {
+    const T x = r * twopi;
+    c0 = kcos(x);
+    s0 = ksin(x);
+  } else {
+    const T x = ((T)0.25 - r) * twopi;  // exact difference
+    c0 = ksin(x);
+    s0 = kcos(x);
+  }
+  // rotate by q quarter turns
+  if (q == 0) { *c = c0; *s = s0; }
+  else if (q == 1) { *c = -s0; *s = c0; }
+  else if (q == 2) { *c = -c0; *s = -s0; }
+  else { *c = s0; *s = -c0; }
 }
 
-// ---- standard normal (Box-Muller, cosine branch) and Exp1 ------------------
-template <class T> GM_HD T normal_from(u32x4 x) {
-  const T u1 = Unif<T>::oc(x.x, x.y);          // (0,1]
-  const T u2 = Unif<T>::co(x.z, x.w);          // [0,1)
-  const T r = gsqrt((T)-2.0 * glog(u1));
-  return r * cos2pi<T>(u2);
+// ---- blocked draws ---------------------------------------------------------
+template <class T> struct Blk;  // draws per Philox block
+template <> struct Blk<float> { static constexpr int S = 4; };
+template <> struct Blk<double> { static constexpr int S = 2; };
+
+GM_HD u32x4 draw_block(uint64_t seed, uint32_t chain, uint64_t blk, uint32_t tag, uint32_t idx) {
+  u32x4 c{idx, chain, (uint32_t)blk, tag | ((uint32_t)(blk >> 32) << 8)};
+  return philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
+
+// the S normals of a block
+GM_HD void normals_of(u32x4 x, float (&z)[4]) {
+  float c, s;
+  const float r0 = gsqrt(-2.0f * glog(Unif<float>::oc(x.x, 0)));
+  sincos2pi<float>(Unif<float>::co(x.y, 0), &c, &s);
+  z[0] = r0 * c;
+  z[1] = r0 * s;
+  const float r1 = gsqrt(-2.0f * glog(Unif<float>::oc(x.z, 0)));
+  sincos2pi<float>(Unif<float>::co(x.w, 0), &c, &s);
+  z[2] = r1 * c;
+  z[3] = r1 * s;
+}
+GM_HD void normals_of(u32x4 x, double (&z)[2]) {
+  double c, s;
+  const double r0 = gsqrt(-2.0 * glog(Unif<double>::oc(x.x, x.y)));
+  sincos2pi<double>(Unif<double>::co(x.z, x.w), &c, &s);
+  z[0] = r0 * c;
+  z[1] = r0 * s;
+}
+// the S uniforms of a block, [0,1) form
+GM_HD void uniforms_of(u32x4 x, float (&u)[4]) {
+  u[0] = Unif<float>::co(x.x, 0);
+  u[1] = Unif<float>::co(x.y, 0);
+  u[2] = Unif<float>::co(x.z, 0);
+  u[3] = Unif<float>::co(x.w, 0);
+}
+GM_HD void uniforms_of(u32x4 x, double (&u)[2]) {
+  u[0] = Unif<double>::co(x.x, x.y);
+  u[1] = Unif<double>::co(x.z, x.w);
+}
+GM_HD float uniform_oc_k(u32x4 x, int k, float) {
+  const uint32_t w = k == 0 ? x.x : k == 1 ? x.y : k == 2 ? x.z : x.w;
+  return Unif<float>::oc(w, 0);
+}
+GM_HD double uniform_oc_k(u32x4 x, int k, double) {
+  return k == 0 ? Unif<double>::oc(x.x, x.y) : Unif<double>::oc(x.z, x.w);
+}
+
+template <class T, int N> GM_HD T pick(const T (&v)[N], int k) {
+  T r = v[0];
+#pragma unroll
+  for (int i = 1; i < N; ++i) r = (k == i) ? v[i] : r;
+  return r;
+}
+
+// single draws (no caching)
 template <class T> GM_HD T normal(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
-  return normal_from<T>(draw(seed, chain, step, tag, idx));
+  T z[Blk<T>::S];
+  normals_of(draw_block(seed, chain, step / Blk<T>::S, tag, idx), z);
+  return pick(z, (int)(step % Blk<T>::S));
 }
 template <class T> GM_HD T uniform_co(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
-  const u32x4 x = draw(seed, chain, step, tag, idx);
-  return Unif<T>::co(x.x, x.y);
+  T u[Blk<T>::S];
+  uniforms_of(draw_block(seed, chain, step / Blk<T>::S, tag, idx), u);
+  return pick(u, (int)(step % Blk<T>::S));
 }
 template <class T> GM_HD T uniform_oc(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
-  const u32x4 x = draw(seed, chain, step, tag, idx);
-  return Unif<T>::oc(x.x, x.y);
+  return uniform_oc_k(draw_block(seed, chain, step / Blk<T>::S, tag, idx), (int)(step % Blk<T>::S), (T)0);
 }
 template <class T> GM_HD T exp1(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
   return -glog(uniform_oc<T>(seed, chain, step, tag, idx));
 }
+
+// A per-lane cache of one block of draws for consecutive steps.
+template <class T> struct NormalCache {
+  T z[Blk<T>::S];
+  uint64_t blk = ~0ull;
+  GM_HD T get(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+    const uint64_t b = step / Blk<T>::S;
+    if (b != blk) {
+      normals_of(draw_block(seed, chain, b, tag, idx), z);
+      blk = b;
+    }
+    return pick(z, (int)(step % Blk<T>::S));
+  }
+};
+template <class T> struct UniformCache {
+  T u[Blk<T>::S];
+  uint64_t blk = ~0ull;
+  GM_HD T get(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+    const uint64_t b = step / Blk<T>::S;
+    if (b != blk) {
+      uniforms_of(draw_block(seed, chain, b, tag, idx), u);
+      blk = b;
+    }
+    return pick(u, (int)(step % Blk<T>::S));
+  }
+};
 
 }  // namespace gm

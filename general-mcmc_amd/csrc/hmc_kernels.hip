@@ -40,6 +40,8 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg) {
   }
   T lp = tg.template eval<LPC, E, true>(q, g, lane);
   long long acc = 0;
+  NormalCache<T> ncache[E];  // one Philox block serves Blk<T>::S transitions
+  UniformCache<T> ucache;
 
   for (int s = 0; s < a.n_steps; ++s) {
     const uint64_t st = a.step0 + (uint64_t)s;
@@ -48,7 +50,7 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
-      p[e] = (i < D) ? normal<T>(a.seed, cid, st, TAG_MOM, (uint32_t)i) : (T)0;
+      p[e] = (i < D) ? ncache[e].get(a.seed, cid, st, TAG_MOM, (uint32_t)i) : (T)0;
       const T sq = p[e] * p[e];
       kp = (e == 0) ? sq : kp + sq;
     }
@@ -83,7 +85,7 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg) {
     const T ke1 = group_sum<LPC>(kq) * (T)0.5;
     // 7-9. Metropolis accept (NaN log_alpha rejects)
     const T log_alpha = (lp1 - lp) + (ke0 - ke1);
-    const T lnu = glog(uniform_co<T>(a.seed, cid, st, TAG_ACC, 0u));
+    const T lnu = glog(ucache.get(a.seed, cid, st, TAG_ACC, 0u));
     if (log_alpha >= lnu) {
 #pragma unroll
       for (int e = 0; e < E; ++e) {

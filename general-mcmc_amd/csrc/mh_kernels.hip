@@ -37,6 +37,8 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg) {
   }
   T lp = tg.template eval<LPC, E, true>(x, gdummy, lane);
   long long acc = 0;
+  NormalCache<T> ncache[E];
+  UniformCache<T> ucache;
   for (int s = 0; s < a.n_steps; ++s) {
     const uint64_t st = a.step0 + (uint64_t)s;
     T qpart = (T)0;
@@ -44,7 +46,7 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg) {
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
       if (i < D) {
-        const T n = normal<T>(a.seed, cid, st, TAG_MH_PROP, (uint32_t)i);
+        const T n = ncache[e].get(a.seed, cid, st, TAG_MH_PROP, (uint32_t)i);
         y[e] = x[e] + n * sd;
       } else {
         y[e] = (T)0;
@@ -56,7 +58,7 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg) {
     const T logq = group_sum<LPC>(qpart) + qconst;
     const T lp1 = tg.template eval<LPC, E, true>(y, gdummy, lane);
     const T log_alpha = (lp1 + logq) - (lp + logq);
-    const T lnu = glog(uniform_co<T>(a.seed, cid, st, TAG_MH_ACC, 0u));
+    const T lnu = glog(ucache.get(a.seed, cid, st, TAG_MH_ACC, 0u));
     if (log_alpha > lnu) {
 #pragma unroll
       for (int e = 0; e < E; ++e) x[e] = y[e];

@@ -207,6 +207,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg) {
   if (a.t0 == 0) record(0);
 
   long long acc = 0, nlf = 0;
+  NormalCache<T> ncache[E];
   for (int s = 0; s < a.n_steps; ++s) {
     const uint64_t st = a.step0 + (uint64_t)s;
     const long long m = a.m0 + s + 1;
@@ -215,7 +216,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
-      p0[e] = (i < D) ? normal<T>(a.seed, cid, st, TAG_NUTS_MOM, (uint32_t)i) : (T)0;
+      p0[e] = (i < D) ? ncache[e].get(a.seed, cid, st, TAG_NUTS_MOM, (uint32_t)i) : (T)0;
     }
     const T logp0 = tg.template eval<LPC, E, true>(q, g0, lane);
     const T joint0 = logp0 - kinetic<LPC, E>(p0);

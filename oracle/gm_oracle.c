@@ -39,13 +39,6 @@ void or_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-static void draw(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx,
-                 uint32_t out[4]) {
-  uint32_t ctr[4] = {idx, chain, (uint32_t)step, tag | ((uint32_t)(step >> 32) << 8)};
-  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-  or_philox(ctr, key, out);
-}
-
 static uint64_t bits_d(double x) { uint64_t u; memcpy(&u, &x, 8); return u; }
 static double from_bits_d(uint64_t u) { double x; memcpy(&x, &u, 8); return x; }
 static uint32_t bits_f(float x) { uint32_t u; memcpy(&u, &x, 4); return u; }
@@ -191,60 +184,81 @@ static float kcos_f(float x) {
   float z = x * x;
   return 1.0f - 0.5f * z + z * z * (4.1666667908e-02f + z * (-1.3888889225e-03f + z * (2.4801587642e-05f + z * -2.7557314297e-07f)));
 }
-double or_cos2pi_d(double u) {
+/* sin and cos of 2 pi u for u in [0,1): quadrant q = floor(4u), r = u - q/4
+ * (exact); first octant direct kernels, second octant complements; rotate. */
+static void sincos2pi_d(double u, double* c, double* s) {
   const double twopi = 6.283185307179586476925286766559;
-  double a = u;
-  if (a > 0.5) a = 1.0 - a;
-  double sign = 1.0;
-  if (a > 0.25) { a = 0.5 - a; sign = -1.0; }
-  double r = (a <= 0.125) ? kcos_d(a * twopi) : ksin_d((0.25 - a) * twopi);
-  return sign * r;
+  const int q = (int)(u * 4.0);
+  const double r = u - (double)q * 0.25;
+  double c0, s0;
+  if (r <= 0.125) { c0 = kcos_d(r * twopi); s0 = ksin_d(r * twopi); }
+  else { double x = (0.25 - r) * twopi; c0 = ksin_d(x); s0 = kcos_d(x); }
+  if (q == 0) { *c = c0; *s = s0; }
+  else if (q == 1) { *c = -s0; *s = c0; }
+  else if (q == 2) { *c = -c0; *s = -s0; }
+  else { *c = s0; *s = -c0; }
 }
-float or_cos2pi_f(float u) {
+static void sincos2pi_f(float u, float* c, float* s) {
   const float twopi = (float)6.283185307179586476925286766559;
-  float a = u;
-  if (a > 0.5f) a = 1.0f - a;
-  float sign = 1.0f;
-  if (a > 0.25f) { a = 0.5f - a; sign = -1.0f; }
-  float r = (a <= 0.125f) ? kcos_f(a * twopi) : ksin_f((0.25f - a) * twopi);
-  return sign * r;
+  const int q = (int)(u * 4.0f);
+  const float r = u - (float)q * 0.25f;
+  float c0, s0;
+  if (r <= 0.125f) { c0 = kcos_f(r * twopi); s0 = ksin_f(r * twopi); }
+  else { float x = (0.25f - r) * twopi; c0 = ksin_f(x); s0 = kcos_f(x); }
+  if (q == 0) { *c = c0; *s = s0; }
+  else if (q == 1) { *c = -s0; *s = c0; }
+  else if (q == 2) { *c = -c0; *s = -s0; }
+  else { *c = s0; *s = -c0; }
 }
+double or_cos2pi_d(double u) { double c, s; sincos2pi_d(u, &c, &s); return c; }
+float or_cos2pi_f(float u) { float c, s; sincos2pi_f(u, &c, &s); return c; }
 
+/* Stream spec v2: a block x = philox({idx, chain, blk, tag | blk_hi << 8}, seed),
+ * blk = step / S (S = 4 for f32 draws, 2 for f64 draws), serves S steps. */
+static void block(uint64_t seed, uint32_t chain, uint64_t blk, uint32_t tag, uint32_t idx,
+                  uint32_t out[4]) {
+  uint32_t ctr[4] = {idx, chain, (uint32_t)blk, tag | ((uint32_t)(blk >> 32) << 8)};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  or_philox(ctr, key, out);
+}
 double or_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
   uint32_t x[4];
-  draw(seed, chain, step, tag, idx, x);
-  double u1 = unif_oc_d(x[0], x[1]);
-  double u2 = unif_co_d(x[2], x[3]);
-  double r = sqrt(-2.0 * or_log_d(u1));
-  return r * or_cos2pi_d(u2);
+  block(seed, chain, step / 2, tag, idx, x);
+  double r = sqrt(-2.0 * or_log_d(unif_oc_d(x[0], x[1])));
+  double c, s;
+  sincos2pi_d(unif_co_d(x[2], x[3]), &c, &s);
+  return (step % 2 == 0) ? r * c : r * s;
 }
 float or_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
   uint32_t x[4];
-  draw(seed, chain, step, tag, idx, x);
-  float u1 = unif_oc_f(x[0]);
-  float u2 = unif_co_f(x[2]);
-  float r = sqrtf(-2.0f * or_log_f(u1));
-  return r * or_cos2pi_f(u2);
+  block(seed, chain, step / 4, tag, idx, x);
+  const int k = (int)(step % 4), pair = k / 2;
+  float r = sqrtf(-2.0f * or_log_f(unif_oc_f(x[2 * pair])));
+  float c, s;
+  sincos2pi_f(unif_co_f(x[2 * pair + 1]), &c, &s);
+  return (k % 2 == 0) ? r * c : r * s;
 }
 double or_uniform_co_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
   uint32_t x[4];
-  draw(seed, chain, step, tag, idx, x);
-  return unif_co_d(x[0], x[1]);
+  block(seed, chain, step / 2, tag, idx, x);
+  const int k = (int)(step % 2);
+  return unif_co_d(x[2 * k], x[2 * k + 1]);
 }
 float or_uniform_co_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
   uint32_t x[4];
-  draw(seed, chain, step, tag, idx, x);
-  return unif_co_f(x[0]);
+  block(seed, chain, step / 4, tag, idx, x);
+  return unif_co_f(x[step % 4]);
 }
 static double uniform_oc_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
   uint32_t x[4];
-  draw(seed, chain, step, tag, idx, x);
-  return unif_oc_d(x[0], x[1]);
+  block(seed, chain, step / 2, tag, idx, x);
+  const int k = (int)(step % 2);
+  return unif_oc_d(x[2 * k], x[2 * k + 1]);
 }
 static float uniform_oc_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
   uint32_t x[4];
-  draw(seed, chain, step, tag, idx, x);
-  return unif_oc_f(x[0]);
+  block(seed, chain, step / 4, tag, idx, x);
+  return unif_oc_f(x[step % 4]);
 }
 
 /* ===================== threading helper ===================== */
