@@ -16,7 +16,6 @@ Prints one JSON line (rank 0).
 from __future__ import annotations
 
 import argparse
-import ctypes as C
 import json
 import os
 import sys
@@ -50,50 +49,31 @@ def parse():
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        # control plane only (barrier, RCCL unique-id broadcast): gloo on the
-        # host, so torch never initialises its own HIP runtime in this process.
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-
     import general_mcmc_amd as gm
     from general_mcmc_amd import _lib
+    from general_mcmc_amd.distributed import Comm, ControlPlane, shard
 
+    cp = ControlPlane()  # gloo control plane when launched by torchrun
+    world, rank = cp.world, cp.rank
     lib = _lib.load()
-    _lib.check(lib.gm_set_device(local))
+    _lib.check(lib.gm_set_device(cp.local_rank))
     lib = _lib.require_gpu()
 
     dtype = np.float32 if a.dtype == "f32" else np.float64
     s_bytes = np.dtype(dtype).itemsize
-    C_loc, D, L = a.chains, a.dim, a.leapfrog
-    C_glob = C_loc * world
-    offset = rank * C_loc
+    D, L = a.dim, a.leapfrog
+    C_glob = a.chains * world
+    offset, C_loc = shard(C_glob, world, rank)
     x0 = gm.init_with_seed(C_glob, D, 42, np.float64)[offset:offset + C_loc].astype(dtype)
     sampler = gm.HMC(gm.RosenbrockND(), x0, a.eps, L, dtype=dtype, chain_offset=offset).set_seed(42)
     if a.layout:
         sampler.set_layout(*[int(v) for v in a.layout.split(",")])
     lanes, elems = sampler.layout()
-
-    comm = None
-    if world > 1:
-        uid = (C.c_char * _lib.UNIQUE_ID_BYTES)()
-        if rank == 0:
-            _lib.check(lib.gm_comm_get_unique_id(uid))
-        obj = [bytes(uid)]
-        dist.broadcast_object_list(obj, src=0)
-        uid = (C.c_char * _lib.UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
-        h = C.c_void_p()
-        _lib.check(lib.gm_comm_init(uid, world, rank, C.byref(h)))
-        comm = h
+    comm = Comm(cp, lib) if world > 1 else None
 
     def barrier_sync():
         _lib.check(lib.gm_device_synchronize())
-        if dist is not None:
-            dist.barrier()
+        cp.barrier()
 
     # warmup = burn-in transitions (untimed)
     if a.warmup > 0:
@@ -104,26 +84,12 @@ def main():
     barrier_sync()
     t_local = time.perf_counter() - t0
     kernel_ms, launches = sampler.last_run_stats()
-
-    if dist is not None:
-        import torch
-        t = torch.tensor([t_local, kernel_ms / max(launches, 1)], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_max, launch_ms = float(t[0]), float(t[1])
-    else:
-        t_max, launch_ms = t_local, kernel_ms / max(launches, 1)
+    t_max, launch_ms = cp.max([t_local, kernel_ms / max(launches, 1)])
 
     # diagnostics on the collected draws (device; RCCL all-gather when N > 1)
     td0 = time.perf_counter()
     if a.steps >= 4:
-        if comm is not None:
-            rhat = np.empty(D, dtype=np.float32)
-            ess = np.empty(D, dtype=np.float32)
-            _lib.check(lib.gm_split_rhat_ess_dist(comm, C.c_void_p(ds.ptr), _lib.dtype_code(dtype),
-                                                  C_loc, a.steps, D, D, C_loc * D, 1,
-                                                  _lib.ptr(rhat), _lib.ptr(ess)))
-        else:
-            rhat, ess = ds.split_rhat_ess()
+        rhat, ess = comm.split_rhat_ess(ds) if comm is not None else ds.split_rhat_ess()
     else:
         rhat = ess = np.full(D, np.nan, dtype=np.float32)
     t_diag = time.perf_counter() - td0
@@ -189,10 +155,9 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if comm is not None:
-        lib.gm_comm_destroy(comm)
+        comm.close()
     sampler.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    cp.close()
 
 
 def cpu_baseline(gm, a, dtype, x0, lanes, elems):
