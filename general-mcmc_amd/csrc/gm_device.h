@@ -42,13 +42,49 @@ enum : int {
   DPP_WAVE_SHR1 = 0x138   // lane l <- lane l-1
 };
 
+// Row broadcasts with a row mask: rows outside ROWMASK receive 0.
+template <int CTRL, int ROWMASK> __device__ __forceinline__ float dpp_rows(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               ROWMASK, 0xf, false));
+}
+template <int CTRL, int ROWMASK> __device__ __forceinline__ double dpp_rows(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, ROWMASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, ROWMASK, 0xf, false);
+  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+template <int CTRL, int ROWMASK> __device__ __forceinline__ int dpp_rows(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWMASK, 0xf, false);
+}
+enum : int { DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143 };
+
+__device__ __forceinline__ float lane63(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+__device__ __forceinline__ int lane63(int v) { return __builtin_amdgcn_readlane(v, 63); }
+__device__ __forceinline__ double lane63(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, 63);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), 63);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
 template <int LPC, class T> __device__ __forceinline__ T group_sum(T v) {
   if constexpr (LPC >= 2) v = v + dpp<DPP_QUAD_XOR1>(v);
   if constexpr (LPC >= 4) v = v + dpp<DPP_QUAD_XOR2>(v);
   if constexpr (LPC >= 8) v = v + dpp<DPP_ROW_HALF_MIRROR>(v);
   if constexpr (LPC >= 16) v = v + dpp<DPP_ROW_MIRROR>(v);
-  if constexpr (LPC >= 32) v = v + __shfl_xor(v, 16, 64);
-  if constexpr (LPC >= 64) v = v + __shfl_xor(v, 32, 64);
+  if constexpr (LPC == 32) v = v + __shfl_xor(v, 16, 64);
+  if constexpr (LPC >= 64) {
+    // Every lane of row r now holds the row total r_r. Rows 1 and 3 add the
+    // broadcast of rows 0 and 2 (r1+r0, r3+r2), then row 3 adds row 1's value:
+    // lane 63 = (r3+r2) + (r1+r0), bitwise the l^16, l^32 stage result
+    // (r0+r1)+(r2+r3) since IEEE addition commutes. The total comes back
+    // wave-uniform (one chain per wave).
+    v = v + dpp_rows<DPP_ROW_BCAST15, 0xa>(v);
+    v = v + dpp_rows<DPP_ROW_BCAST31, 0x8>(v);
+    v = lane63(v);
+  }
   return v;
 }
 // lane l receives lane l+1's value. Wave-wide DPP shift: at a group's last
@@ -64,6 +100,24 @@ template <int LPC, class T> __device__ __forceinline__ T from_prev(T v) {
   else return dpp<DPP_WAVE_SHR1>(v);
 }
 
+// Branch-free "c ? v : +0" with a per-lane mask the compiler cannot see
+// through (an empty asm), so it stays one v_and per use instead of being
+// turned back into a select and then into a divergent branch around the
+// guarded arithmetic.
+template <class T> struct MaskOf;
+template <> struct MaskOf<float> { using type = uint32_t; };
+template <> struct MaskOf<double> { using type = uint64_t; };
+template <class T> __device__ __forceinline__ typename MaskOf<T>::type lane_mask(bool c) {
+  using M = typename MaskOf<T>::type;
+  M m = c ? ~(M)0 : (M)0;
+  asm("" : "+v"(m));
+  return m;
+}
+template <class T> __device__ __forceinline__ T keep(T v, typename MaskOf<T>::type m) {
+  using M = typename MaskOf<T>::type;
+  return __builtin_bit_cast(T, __builtin_bit_cast(M, v) & m);
+}
+
 // ---------------------------------------------------------------------------
 // Rosenbrock: logp = -sum_{i<=D-2} [ b*(x_{i+1}-x_i^2)^2 + (a-x_i)^2 ]
 // RosenbrockND (distributions.rs:544-554) is a=1, b=100; Rosenbrock2D
@@ -72,32 +126,51 @@ template <int LPC, class T> __device__ __forceinline__ T from_prev(T v) {
 //   g_i = A_i - B_i,  A_i = [i<=D-2] ( (4b x_i) t_i + 2 (a - x_i) ),
 //                     B_i = [1<=i<=D-1] (2b t_{i-1}),   t_i = x_{i+1} - x_i^2
 // ([.] selects +0 when false).
+template <class T, int E> struct RosenbrockLane;
 template <class T> struct RosenbrockT {
   T a, b, b2, b4;  // b2 = 2b, b4 = 4b (rounded once, host side)
   int D;
-  template <int LPC, int E, bool LOGP>
-  __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int lane) const {
+  // per-lane view with the coordinate masks computed once per kernel
+  template <int LPC, int E> __device__ __forceinline__ RosenbrockLane<T, E> bind(int lane) const {
+    RosenbrockLane<T, E> r;
+    r.a = a; r.b = b; r.b2 = b2; r.b4 = b4;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      r.ms[e] = lane_mask<T>(i <= D - 2);
+      r.mp[e] = lane_mask<T>((i >= 1) & (i <= D - 1));
+    }
+    return r;
+  }
+};
+template <class T, int E> struct RosenbrockLane {
+  T a, b, b2, b4;
+  typename MaskOf<T>::type ms[E], mp[E];  // [i <= D-2], [1 <= i <= D-1]
+  template <int LPC, int E_, bool LOGP>
+  __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int) const {
+    static_assert(E_ == E, "layout mismatch");
     T t[E];
+    // Both lane shifts read x only: t_{i-1} for a group's first slot is
+    // recomputed from x_{i-1} (the operands lane i-1 uses, so the same bits)
+    // instead of being shifted out of t, which keeps one DPP off the chain.
     const T nx = from_next<LPC>(x[0]);
+    const T px = from_prev<LPC>(x[E - 1]);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const T xn = (e + 1 < E) ? x[(e + 1 < E) ? e + 1 : e] : nx;
       t[e] = xn - x[e] * x[e];
     }
-    const T tp = from_prev<LPC>(t[E - 1]);
+    const T tp = x[0] - px * px;
     T part = (T)0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int i = lane * E + e;
-      const bool hs = i <= D - 2;
-      const bool hp = (i >= 1) & (i <= D - 1);
       const T tprev = (e > 0) ? t[(e > 0) ? e - 1 : 0] : tp;
       const T am = a - x[e];
-      const T A = hs ? (b4 * x[e]) * t[e] + (T)2 * am : (T)0;
-      const T B = hp ? b2 * tprev : (T)0;
+      const T A = keep((b4 * x[e]) * t[e] + (T)2 * am, ms[e]);
+      const T B = keep(b2 * tprev, mp[e]);
       g[e] = A - B;
       if (LOGP) {
-        const T s = hs ? (b * (t[e] * t[e]) + am * am) : (T)0;
+        const T s = keep(b * (t[e] * t[e]) + am * am, ms[e]);
         part = (e == 0) ? s : part + s;
       }
     }
@@ -111,6 +184,7 @@ template <class T> struct RosenbrockT {
 template <class T> struct IsoGaussT {
   T var;  // std*std
   int D;
+  template <int LPC, int E> __device__ __forceinline__ IsoGaussT bind(int) const { return *this; }
   template <int LPC, int E, bool LOGP>
   __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int lane) const {
     T part = (T)0;
@@ -136,6 +210,7 @@ template <class T> struct GaussT {
   const T* prec;  // [D*D] device row-major
   T nc;
   int D;
+  template <int LPC, int E> __device__ __forceinline__ GaussT bind(int) const { return *this; }
   template <int LPC, int E, bool LOGP>
   __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int lane) const {
     T d[E], w[E];

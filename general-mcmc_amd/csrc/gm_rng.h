@@ -66,8 +66,10 @@ GM_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
 GM_HD u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = mulhi32(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = mulhi32(0xCD9E8D57u, c.z);
+    // one 32x32->64 product per multiplier (a single v_mad_u64_u32 on gfx950)
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -192,6 +194,56 @@ GM_HD float glog(float x) {
   return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
 }
 
+// The same polynomials restricted to a positive normal finite x (no special
+// cases: the uniforms fed to it are >= 2^-24 for f32 and >= 2^-53 for f64),
+// identical bits to glog on that domain; branch-free.
+GM_HD double glog_pos(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+               Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  const uint64_t u = d2u(x);
+  int k = (int)(u >> 52) - 1023;
+  double m = u2d((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+  const bool big = m > 1.4142135623730951;
+  m = big ? m * 0.5 : m;
+  k += big ? 1 : 0;
+  const double f = m - 1.0;
+  const double s = f / (2.0 + f);
+  const double z = s * s, w = z * z;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)k;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+GM_HD float glog_pos(float x) {
+  const float ln2_hi = 6.9313812256e-01f, ln2_lo = 9.0580006145e-06f;
+  const float Lg1 = 0.66666662693f, Lg2 = 0.40000972152f, Lg3 = 0.28498786688f, Lg4 = 0.24279078841f;
+  const uint32_t u = f2u(x);
+  int k = (int)(u >> 23) - 127;
+  float m = u2f((u & 0x007fffffu) | 0x3f800000u);
+  const bool big = m > 1.41421353816986083984f;
+  m = big ? m * 0.5f : m;
+  k += big ? 1 : 0;
+  const float f = m - 1.0f;
+  const float s = f / (2.0f + f);
+  const float z = s * s, w = z * z;
+  const float t1 = w * (Lg2 + w * Lg4);
+  const float t2 = z * (Lg1 + w * Lg3);
+  const float R = t2 + t1;
+  const float hfsq = 0.5f * f * f;
+  const float dk = (float)k;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+// log of a [0,1) uniform: glog_pos, or -inf at 0 (the only special input).
+template <class T> GM_HD T glog_unif(T u) {
+  const T l = glog_pos(u);
+  return (u == (T)0) ? (T)(-u2d(0x7ff0000000000000ull)) : l;
+}
+
 // ---- exp (FreeBSD msun e_exp.c / e_expf.c) -----------------------------------
 GM_HD double scale2(double y, int k) {  // y * 2^k, y in [0.5, 2]
   if (k > 1023) return y * u2d(0x7fe0000000000000ull) * u2d((uint64_t)(k - 1023 + 1023) << 52);
@@ -273,21 +325,16 @@ template <class T> GM_HD void sincos2pi(T u, T* c, T* s) {
   const T f4 = u * (T)4;
   const int q = (int)f4;          // u in [0,1): q in 0..3
   const T r = u - (T)q * (T)0.25;  // exact
-  T c0, s0;
-  if (r <= (T)0.125) {
-    const T x = r * twopi;
-    c0 = kcos(x);
-    s0 = ksin(x);
-  } else {
-    const T x = ((T)0.25 - r) * twopi;  // exact difference
-    c0 = ksin(x);
-    s0 = kcos(x);
-  }
-  // rotate by q quarter turns
-  if (q == 0) { *c = c0; *s = s0; }
-  else if (q == 1) { *c = -s0; *s = c0; }
-  else if (q == 2) { *c = -c0; *s = -s0; }
-  else { *c = s0; *s = -c0; }
+  // branch-free: the same kernels on the same argument, then selects
+  const bool lo = r <= (T)0.125;
+  const T x = lo ? r * twopi : ((T)0.25 - r) * twopi;  // exact difference
+  const T kc = kcos(x), ks = ksin(x);
+  const T c0 = lo ? kc : ks, s0 = lo ? ks : kc;
+  // rotate by q quarter turns: q=1 (-s0, c0), q=2 (-c0, -s0), q=3 (s0, -c0)
+  const bool odd = (q & 1) != 0;
+  const T cc = odd ? s0 : c0, ss = odd ? c0 : s0;
+  *c = (q == 1 || q == 2) ? -cc : cc;
+  *s = (q >= 2) ? -ss : ss;
 }
 
 // ---- blocked draws ---------------------------------------------------------
@@ -303,18 +350,18 @@ GM_HD u32x4 draw_block(uint64_t seed, uint32_t chain, uint64_t blk, uint32_t tag
 // the S normals of a block
 GM_HD void normals_of(u32x4 x, float (&z)[4]) {
   float c, s;
-  const float r0 = gsqrt(-2.0f * glog(Unif<float>::oc(x.x, 0)));
+  const float r0 = gsqrt(-2.0f * glog_pos(Unif<float>::oc(x.x, 0)));
   sincos2pi<float>(Unif<float>::co(x.y, 0), &c, &s);
   z[0] = r0 * c;
   z[1] = r0 * s;
-  const float r1 = gsqrt(-2.0f * glog(Unif<float>::oc(x.z, 0)));
+  const float r1 = gsqrt(-2.0f * glog_pos(Unif<float>::oc(x.z, 0)));
   sincos2pi<float>(Unif<float>::co(x.w, 0), &c, &s);
   z[2] = r1 * c;
   z[3] = r1 * s;
 }
 GM_HD void normals_of(u32x4 x, double (&z)[2]) {
   double c, s;
-  const double r0 = gsqrt(-2.0 * glog(Unif<double>::oc(x.x, x.y)));
+  const double r0 = gsqrt(-2.0 * glog_pos(Unif<double>::oc(x.x, x.y)));
   sincos2pi<double>(Unif<double>::co(x.z, x.w), &c, &s);
   z[0] = r0 * c;
   z[1] = r0 * s;
@@ -360,7 +407,7 @@ template <class T> GM_HD T uniform_oc(uint64_t seed, uint32_t chain, uint64_t st
   return uniform_oc_k(draw_block(seed, chain, step / Blk<T>::S, tag, idx), (int)(step % Blk<T>::S), (T)0);
 }
 template <class T> GM_HD T exp1(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
-  return -glog(uniform_oc<T>(seed, chain, step, tag, idx));
+  return -glog_pos(uniform_oc<T>(seed, chain, step, tag, idx));
 }
 
 // A per-lane cache of one block of draws for consecutive steps.
@@ -388,5 +435,18 @@ template <class T> struct UniformCache {
     return pick(u, (int)(step % Blk<T>::S));
   }
 };
+
+// Register-resident draws for a kernel that walks consecutive steps: the
+// block for step st is generated once (at the first step and at each block
+// boundary), then consumed front to back by shifting, so no array is ever
+// indexed by a runtime value (which the compiler would spill to LDS).
+template <class T, int S> GM_HD void shift_front(T (&v)[S]) {
+#pragma unroll
+  for (int i = 0; i + 1 < S; ++i) v[i] = v[i + 1];
+}
+// drop the first k slots (k = st % S when a walk starts mid-block)
+template <class T, int S> GM_HD void skip_front(T (&v)[S], int k) {
+  for (int j = 0; j < k; ++j) shift_front(v);
+}
 
 }  // namespace gm

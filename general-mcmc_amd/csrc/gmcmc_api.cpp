@@ -11,6 +11,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
@@ -431,6 +432,24 @@ int gm_sampler_last_run_stats(gm_sampler* s, double* kernel_ms, int64_t* launche
 
 // Runs `total` transitions; transitions with index >= collect_from (0-based
 // within this call) are stored at sample rows (index - collect_from).
+// Leapfrog-loop unroll of the HMC kernel (a tuning knob with identical
+// results; GM_HMC_UNROLL=1|4 overrides the default for measurements).
+// Measured (tools/probe_hmc_scaling.py, PROBE_UNROLLS=1,4): x4 is ~12%
+// faster while the grid has at most one wave per SIMD (latency bound), and
+// 10-20% slower from two waves per SIMD up.
+static int hmc_lf_unroll(long long waves) {
+  const char* v = getenv("GM_HMC_UNROLL");
+  if (v) return atoi(v) == 4 ? 4 : 1;
+  static const int simds = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    return 4 * cus;
+  }();
+  return waves <= simds ? 4 : 1;
+}
+
 static int run_steps(gm_sampler* s, long long total, long long collect_from, int progress) {
   GM_HIP(hipSetDevice(s->device));
   s->last_ms = 0;
@@ -477,6 +496,7 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
       a.n_steps = (int)n;
       a.collect_from = (int)cf;
       a.sample_row0 = row0;
+      a.lf_unroll = hmc_lf_unroll((s->C * s->lay.lanes + 63) / 64);
       e = launch_hmc(s->dt, s->tg, s->lay, a, s->stream);
     } else {
       MhLaunch a;

@@ -21,16 +21,20 @@
 namespace gm {
 
 template <class T, int LPC, int E, class TG>
-__global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg) {
+__global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
   const int lane = (int)(gtid % LPC);
+  const auto tg = tg_.template bind<LPC, E>(lane);  // per-lane target view
   if (c >= a.C) return;  // whole lane groups leave together
   const int D = a.D;
   T* __restrict__ qs = (T*)a.q;
   const T eps = (T)a.eps;
   const T half = (T)0.5 * eps;  // batched_hmc.rs:167
   const uint32_t cid = a.chain_offset + (uint32_t)c;
+  // wave-uniform chain id when one chain fills the wave: the per-chain draws
+  // (accept uniform) then run on the scalar unit
+  const uint32_t ucid = (LPC == 64) ? (uint32_t)__builtin_amdgcn_readfirstlane((int)cid) : cid;
 
   T q[E], g[E], p[E], q1[E], p1[E], g1[E];
 #pragma unroll
@@ -40,22 +44,53 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg) {
   }
   T lp = tg.template eval<LPC, E, true>(q, g, lane);
   long long acc = 0;
-  NormalCache<T> ncache[E];  // one Philox block serves Blk<T>::S transitions
-  UniformCache<T> ucache;
+  constexpr int S = Blk<T>::S;  // one Philox block serves S transitions
+  T zs[E][S];                   // momentum draws of the current block, front = this step
+  T kes[S];                     // their kinetic energies
+  T lus[S];                     // ln u of the accept uniforms
 
   for (int s = 0; s < a.n_steps; ++s) {
     const uint64_t st = a.step0 + (uint64_t)s;
-    // 1. momentum ~ N(0, I)
-    T kp = (T)0;
+    if (s == 0 || st % S == 0) {
+      // Refill: S momentum vectors, their S kinetic energies (S independent
+      // reductions) and the S accept log-uniforms, all off the per-step path.
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        normals_of(draw_block(a.seed, cid, st / S, TAG_MOM, (uint32_t)i), zs[e]);
+#pragma unroll
+        for (int k = 0; k < S; ++k) zs[e][k] = (i < D) ? zs[e][k] : (T)0;
+      }
+#pragma unroll
+      for (int k = 0; k < S; ++k) {
+        T kp = (T)0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const T sq = zs[e][k] * zs[e][k];
+          kp = (e == 0) ? sq : kp + sq;
+        }
+        kes[k] = group_sum<LPC>(kp) * (T)0.5;  // 2. kinetic energy
+      }
+      T us[S];
+      uniforms_of(draw_block(a.seed, ucid, st / S, TAG_ACC, 0u), us);
+#pragma unroll
+      for (int k = 0; k < S; ++k) lus[k] = glog_unif(us[k]);
+      const int k0 = (int)(st % S);
+#pragma unroll
+      for (int e = 0; e < E; ++e) skip_front(zs[e], k0);
+      skip_front(kes, k0);
+      skip_front(lus, k0);
+    }
+    // 1. momentum ~ N(0, I) and its kinetic energy: front of the block
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int i = lane * E + e;
-      p[e] = (i < D) ? ncache[e].get(a.seed, cid, st, TAG_MOM, (uint32_t)i) : (T)0;
-      const T sq = p[e] * p[e];
-      kp = (e == 0) ? sq : kp + sq;
+      p[e] = zs[e][0];
+      shift_front(zs[e]);
     }
-    // 2. kinetic energy
-    const T ke0 = group_sum<LPC>(kp) * (T)0.5;
+    const T ke0 = kes[0];
+    const T lnu = lus[0];
+    shift_front(kes);
+    shift_front(lus);
     // 4. proposal buffers
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -63,15 +98,37 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg) {
       p1[e] = p[e];
       g1[e] = g[e];
     }
-    // 5. leapfrog
+    // 5. leapfrog: L-1 gradient-only steps, then the last one with logp.
+    // gh = g*(0.5 eps) is shared by the closing kick of one step and the
+    // opening kick of the next (same operands, same bits).
     T lp1 = lp;
-    for (int l = 0; l < a.L; ++l) {
+    T gh[E];
 #pragma unroll
-      for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+    for (int e = 0; e < E; ++e) gh[e] = g1[e] * half;
+    // (unrolled by hand: the DPP intrinsics are convergent, so the compiler
+    // will not runtime-unroll, and a taken branch costs a wave ~20 cycles)
+    auto lf = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) p1[e] = p1[e] + gh[e];
 #pragma unroll
       for (int e = 0; e < E; ++e) q1[e] = q1[e] + p1[e] * eps;
-      if (l + 1 < a.L) tg.template eval<LPC, E, false>(q1, g1, lane);
-      else lp1 = tg.template eval<LPC, E, true>(q1, g1, lane);
+      tg.template eval<LPC, E, false>(q1, g1, lane);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        gh[e] = g1[e] * half;
+        p1[e] = p1[e] + gh[e];
+      }
+    };
+    int l = 0;
+    if (a.lf_unroll == 4)
+      for (; l + 4 < a.L; l += 4) { lf(); lf(); lf(); lf(); }
+    for (; l + 1 < a.L; ++l) lf();
+    if (a.L >= 1) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) p1[e] = p1[e] + gh[e];
+#pragma unroll
+      for (int e = 0; e < E; ++e) q1[e] = q1[e] + p1[e] * eps;
+      lp1 = tg.template eval<LPC, E, true>(q1, g1, lane);
 #pragma unroll
       for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
     }
@@ -85,7 +142,6 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg) {
     const T ke1 = group_sum<LPC>(kq) * (T)0.5;
     // 7-9. Metropolis accept (NaN log_alpha rejects)
     const T log_alpha = (lp1 - lp) + (ke0 - ke1);
-    const T lnu = glog(ucache.get(a.seed, cid, st, TAG_ACC, 0u));
     if (log_alpha >= lnu) {
 #pragma unroll
       for (int e = 0; e < E; ++e) {

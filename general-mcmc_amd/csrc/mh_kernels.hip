@@ -15,14 +15,18 @@
 namespace gm {
 
 template <class T, int LPC, int E, class TG>
-__global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg) {
+__global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
   const int lane = (int)(gtid % LPC);
+  const auto tg = tg_.template bind<LPC, E>(lane);  // per-lane target view
   if (c >= a.C) return;
   const int D = a.D;
   T* __restrict__ qs = (T*)a.q;
   const uint32_t cid = a.chain_offset + (uint32_t)c;
+  // wave-uniform chain id when one chain fills the wave: the per-chain draws
+  // (accept uniform) then run on the scalar unit
+  const uint32_t ucid = (LPC == 64) ? (uint32_t)__builtin_amdgcn_readfirstlane((int)cid) : cid;
   const T sd = (T)a.prop_std;
   const T var = sd * sd;
   const T two_var = (T)2 * var;
@@ -58,7 +62,7 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg) {
     const T logq = group_sum<LPC>(qpart) + qconst;
     const T lp1 = tg.template eval<LPC, E, true>(y, gdummy, lane);
     const T log_alpha = (lp1 + logq) - (lp + logq);
-    const T lnu = glog(ucache.get(a.seed, cid, st, TAG_MH_ACC, 0u));
+    const T lnu = glog_unif(ucache.get(a.seed, ucid, st, TAG_MH_ACC, 0u));
     if (log_alpha > lnu) {
 #pragma unroll
       for (int e = 0; e < E; ++e) x[e] = y[e];

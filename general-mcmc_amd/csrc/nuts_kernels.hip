@@ -158,10 +158,11 @@ __device__ T find_reasonable_epsilon(const TG& tg, const T (&q0)[E], const T (&p
 }
 
 template <class T, int LPC, int E, class TG>
-__global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg) {
+__global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
   const int lane = (int)(gtid % LPC);
+  const auto tg = tg_.template bind<LPC, E>(lane);  // per-lane target view
   if (c >= a.C) return;
   const int D = a.D;
   const long long C = a.C;

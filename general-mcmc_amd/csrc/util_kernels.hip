@@ -9,10 +9,11 @@ namespace gm {
 template <class T, int LPC, int E, class TG>
 __global__ __launch_bounds__(256) void logp_grad_kernel(long long n, int D, const T* __restrict__ x,
                                                         T* __restrict__ logp, T* __restrict__ grad,
-                                                        TG tg) {
+                                                        TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
   const int lane = (int)(gtid % LPC);
+  const auto tg = tg_.template bind<LPC, E>(lane);  // per-lane target view
   if (c >= n) return;
   T q[E], g[E];
 #pragma unroll
