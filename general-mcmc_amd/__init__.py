@@ -5,7 +5,7 @@ MH via ChainRunner, split-R-hat/ESS): the same facades and conventions, with
 every transition computed by hand-written gfx950 HIP kernels in libgmcmc.so
 (include/gmcmc.h is the C ABI). There is no CPU fallback.
 """
-from . import _lib
+from . import _lib, batch_vector
 from ._lib import GMError
 from .core import init, init_det, init_with_seed
 from .distributions import (DenseGaussian, DiffableGaussian2D, Gaussian2D, IsotropicGaussian,
@@ -19,4 +19,5 @@ __all__ = [
     "HMC", "NUTS", "NUTSChain", "MetropolisHastings", "RosenbrockND", "Rosenbrock2D",
     "IsotropicGaussian", "DiffableGaussian2D", "DenseGaussian", "Gaussian2D", "init", "init_det",
     "init_with_seed", "split_rhat_mean_ess", "basic_stats", "BasicStats", "RunStats", "GMError",
+    "batch_vector",
 ]

@@ -84,6 +84,25 @@ SIGNATURES = {
     "gm_comm_init": (_ip, [_vp, _i32, _i32, C.POINTER(_vp)]),
     "gm_comm_destroy": (_ip, [_vp]),
     "gm_split_rhat_ess_dist": (_ip, [_vp, _vp, _ip, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
+    # granular BatchVector ops (tier 2)
+    "gm_malloc": (_ip, [C.POINTER(_vp), C.c_size_t]),
+    "gm_free": (_ip, [_vp]),
+    "gm_memcpy_htod": (_ip, [_vp, _vp, C.c_size_t]),
+    "gm_memcpy_dtoh": (_ip, [_vp, _vp, C.c_size_t]),
+    "gm_memcpy_dtod": (_ip, [_vp, _vp, C.c_size_t]),
+    "gm_bv_kinetic_energy": (_ip, [_ip, _i64, _i64, _vp, _vp]),
+    "gm_bv_masked_assign": (_ip, [_ip, _i64, _i64, _vp, _vp, _vp]),
+    "gm_bv_add_scaled_assign": (_ip, [_ip, _i64, _vp, _vp, _dbl]),
+    "gm_bv_fill_random_normal": (_ip, [_ip, _i64, _i64, _vp, _u64, C.c_uint32, _u64]),
+    "gm_bv_sample_uniform": (_ip, [_ip, _i64, _vp, _u64, C.c_uint32, _u64]),
+    "gm_bv_energy_sub": (_ip, [_ip, _i64, _vp, _vp, _vp]),
+    "gm_bv_energy_add": (_ip, [_ip, _i64, _vp, _vp, _vp]),
+    "gm_bv_energy_neg": (_ip, [_ip, _i64, _vp, _vp]),
+    "gm_bv_energy_ln": (_ip, [_ip, _i64, _vp, _vp]),
+    "gm_bv_accept_mask": (_ip, [_ip, _i64, _vp, _vp, _vp]),
+    "gm_bv_target_create": (_ip, [C.POINTER(gm_target), _ip, C.POINTER(_vp)]),
+    "gm_bv_logp_and_grad": (_ip, [_vp, _i64, _vp, _vp, _vp]),
+    "gm_bv_target_destroy": (_ip, [_vp]),
 }
 
 _lib = None

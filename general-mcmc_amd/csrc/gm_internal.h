@@ -72,6 +72,25 @@ hipError_t launch_mh(gm_dtype dt, const TargetDev& tg, const Layout& lay, const 
 hipError_t launch_logp_grad(gm_dtype dt, const TargetDev& tg, const Layout& lay, long long n,
                             const void* x, void* logp, void* grad, hipStream_t st);
 
+// ---- granular BatchVector ops (bv_kernels.hip) -------------------------------
+hipError_t launch_bv_kinetic(gm_dtype dt, const Layout& lay, long long C, int D, const void* p, void* ke,
+                             hipStream_t st);
+hipError_t launch_bv_masked_assign(gm_dtype dt, long long C, int D, void* x, const void* o,
+                                   const uint8_t* mask, hipStream_t st);
+hipError_t launch_bv_axpy(gm_dtype dt, long long n, void* x, const void* o, double alpha, hipStream_t st);
+hipError_t launch_bv_normal(gm_dtype dt, long long C, int D, void* out, uint64_t seed, uint32_t off,
+                            uint64_t step, uint32_t tag, hipStream_t st);
+hipError_t launch_bv_uniform(gm_dtype dt, long long C, void* out, uint64_t seed, uint32_t off, uint64_t step,
+                             uint32_t tag, hipStream_t st);
+hipError_t launch_bv_energy(gm_dtype dt, int op, long long n, const void* a, const void* b, void* out,
+                            hipStream_t st);
+hipError_t launch_bv_accept(gm_dtype dt, long long n, const void* la, const void* lnu, uint8_t* mask,
+                            hipStream_t st);
+
+// target construction (gmcmc_api.cpp): device copies of mean / precision
+int build_target(const gm_target* t, gm_dtype dt, long long dim, TargetDev* out, void** d_mu,
+                 void** d_prec);
+
 // ---- utilities -------------------------------------------------------------
 // [rows][C][D] -> [C][rows][D]
 hipError_t launch_transpose_samples(gm_dtype dt, const void* src, void* dst, long long rows,

@@ -154,8 +154,8 @@ static int upload_as(gm_dtype dt, const double* src, size_t n, void** dst) {
   return GM_OK;
 }
 
-static int build_target(const gm_target* t, gm_dtype dt, long long dim, TargetDev* out, void** d_mu,
-                        void** d_prec) {
+int gm::build_target(const gm_target* t, gm_dtype dt, long long dim, TargetDev* out, void** d_mu,
+                     void** d_prec) {
   GM_REQ(t != nullptr, "target is NULL");
   GM_REQ(t->dim == dim, "target dim does not match the sampler dim");
   GM_REQ(dim >= 1 && dim <= 1024, "dim must be in [1, 1024]");

@@ -1,0 +1,159 @@
+// gmcmc_bv.cpp — C ABI of the granular BatchVector ops (tier 2 of the
+// boundary, include/gmcmc.h): argument checks, then one kernel launch each
+// (bv_kernels.hip) on the null stream.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "gm_internal.h"
+#include "gm_rng.h"
+
+using namespace gm;
+
+#define BV_REQ(cond, msg)  \
+  do {                     \
+    if (!(cond)) {         \
+      set_error(msg);      \
+      return GM_EINVAL;    \
+    }                      \
+  } while (0)
+
+static int bv_status(hipError_t e, const char* what) {
+  if (e == hipSuccess) return GM_OK;
+  set_error(std::string(what) + ": " + hipGetErrorString(e));
+  return GM_EHIP;
+}
+static bool dtype_ok(gm_dtype dt) { return dt == GM_F32 || dt == GM_F64; }
+
+struct gm_bv_target {
+  gm_dtype dt = GM_F32;
+  TargetDev tg;
+  void* d_mu = nullptr;
+  void* d_prec = nullptr;
+};
+
+extern "C" {
+
+int gm_malloc(void** dev_ptr, size_t bytes) {
+  BV_REQ(dev_ptr != nullptr, "dev_ptr is NULL");
+  *dev_ptr = nullptr;
+  if (bytes == 0) return GM_OK;
+  if (hipMalloc(dev_ptr, bytes) != hipSuccess) {
+    *dev_ptr = nullptr;
+    set_error("device allocation failed");
+    return GM_ENOMEM;
+  }
+  return GM_OK;
+}
+int gm_free(void* dev_ptr) { return bv_status(hipFree(dev_ptr), "hipFree"); }
+int gm_memcpy_htod(void* dst, const void* src, size_t bytes) {
+  if (bytes == 0) return GM_OK;
+  BV_REQ(dst && src, "NULL pointer");
+  return bv_status(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
+}
+int gm_memcpy_dtoh(void* dst, const void* src, size_t bytes) {
+  if (bytes == 0) return GM_OK;
+  BV_REQ(dst && src, "NULL pointer");
+  return bv_status(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+}
+int gm_memcpy_dtod(void* dst, const void* src, size_t bytes) {
+  if (bytes == 0) return GM_OK;
+  BV_REQ(dst && src, "NULL pointer");
+  return bv_status(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, nullptr), "hipMemcpy D2D");
+}
+
+int gm_bv_kinetic_energy(gm_dtype dt, int64_t C, int64_t D, const void* p, void* ke) {
+  BV_REQ(dtype_ok(dt), "bad dtype");
+  BV_REQ(C >= 0 && D >= 1 && D <= 1024, "n_chains >= 0 and dim in [1, 1024] required");
+  if (C == 0) return GM_OK;
+  BV_REQ(p && ke, "NULL pointer");
+  const Layout lay = default_layout((int)D, dt, GM_TARGET_ROSENBROCK);
+  return bv_status(launch_bv_kinetic(dt, lay, C, (int)D, p, ke, nullptr), "kinetic_energy");
+}
+int gm_bv_masked_assign(gm_dtype dt, int64_t C, int64_t D, void* x, const void* o, const uint8_t* mask) {
+  BV_REQ(dtype_ok(dt), "bad dtype");
+  BV_REQ(C >= 0 && D >= 1, "bad shape");
+  if (C == 0) return GM_OK;
+  BV_REQ(x && o && mask, "NULL pointer");
+  return bv_status(launch_bv_masked_assign(dt, C, (int)D, x, o, mask, nullptr), "masked_assign");
+}
+int gm_bv_add_scaled_assign(gm_dtype dt, int64_t n, void* x, const void* o, double alpha) {
+  BV_REQ(dtype_ok(dt), "bad dtype");
+  BV_REQ(n >= 0, "bad size");
+  if (n == 0) return GM_OK;
+  BV_REQ(x && o, "NULL pointer");
+  return bv_status(launch_bv_axpy(dt, n, x, o, alpha, nullptr), "add_scaled_assign");
+}
+int gm_bv_fill_random_normal(gm_dtype dt, int64_t C, int64_t D, void* out, uint64_t seed,
+                             uint32_t chain_offset, uint64_t step) {
+  BV_REQ(dtype_ok(dt), "bad dtype");
+  BV_REQ(C >= 0 && D >= 1, "bad shape");
+  if (C == 0) return GM_OK;
+  BV_REQ(out, "NULL pointer");
+  return bv_status(launch_bv_normal(dt, C, (int)D, out, seed, chain_offset, step, TAG_MOM, nullptr),
+                   "fill_random_normal");
+}
+int gm_bv_sample_uniform(gm_dtype dt, int64_t C, void* out, uint64_t seed, uint32_t chain_offset,
+                         uint64_t step) {
+  BV_REQ(dtype_ok(dt), "bad dtype");
+  BV_REQ(C >= 0, "bad size");
+  if (C == 0) return GM_OK;
+  BV_REQ(out, "NULL pointer");
+  return bv_status(launch_bv_uniform(dt, C, out, seed, chain_offset, step, TAG_ACC, nullptr),
+                   "sample_uniform");
+}
+static int energy(int op, gm_dtype dt, int64_t n, const void* a, const void* b, void* out) {
+  BV_REQ(dtype_ok(dt), "bad dtype");
+  BV_REQ(n >= 0, "bad size");
+  if (n == 0) return GM_OK;
+  BV_REQ(a && out && (b || op >= 2), "NULL pointer");
+  return bv_status(launch_bv_energy(dt, op, n, a, b, out, nullptr), "energy op");
+}
+int gm_bv_energy_sub(gm_dtype dt, int64_t n, const void* a, const void* b, void* out) {
+  return energy(0, dt, n, a, b, out);
+}
+int gm_bv_energy_add(gm_dtype dt, int64_t n, const void* a, const void* b, void* out) {
+  return energy(1, dt, n, a, b, out);
+}
+int gm_bv_energy_neg(gm_dtype dt, int64_t n, const void* a, void* out) { return energy(2, dt, n, a, nullptr, out); }
+int gm_bv_energy_ln(gm_dtype dt, int64_t n, const void* a, void* out) { return energy(3, dt, n, a, nullptr, out); }
+int gm_bv_accept_mask(gm_dtype dt, int64_t n, const void* la, const void* lnu, uint8_t* mask) {
+  BV_REQ(dtype_ok(dt), "bad dtype");
+  BV_REQ(n >= 0, "bad size");
+  if (n == 0) return GM_OK;
+  BV_REQ(la && lnu && mask, "NULL pointer");
+  return bv_status(launch_bv_accept(dt, n, la, lnu, mask, nullptr), "accept_mask");
+}
+
+int gm_bv_target_create(const gm_target* target, gm_dtype dt, gm_bv_target** out) {
+  BV_REQ(out != nullptr, "out is NULL");
+  *out = nullptr;
+  BV_REQ(dtype_ok(dt), "bad dtype");
+  BV_REQ(target != nullptr, "target is NULL");
+  gm_bv_target* t = new gm_bv_target();
+  t->dt = dt;
+  const int rc = build_target(target, dt, target->dim, &t->tg, &t->d_mu, &t->d_prec);
+  if (rc) {
+    delete t;
+    return rc;
+  }
+  *out = t;
+  return GM_OK;
+}
+int gm_bv_logp_and_grad(gm_bv_target* t, int64_t C, const void* x, void* grad, void* logp) {
+  BV_REQ(t != nullptr, "target is NULL");
+  BV_REQ(C >= 0, "bad size");
+  if (C == 0) return GM_OK;
+  BV_REQ(x != nullptr, "x is NULL");
+  const Layout lay = default_layout(t->tg.D, t->dt, t->tg.kind);
+  return bv_status(launch_logp_grad(t->dt, t->tg, lay, C, x, logp, grad, nullptr), "logp_and_grad");
+}
+int gm_bv_target_destroy(gm_bv_target* t) {
+  if (!t) return GM_OK;
+  if (t->d_mu) hipFree(t->d_mu);
+  if (t->d_prec) hipFree(t->d_prec);
+  delete t;
+  return GM_OK;
+}
+
+}  // extern "C"

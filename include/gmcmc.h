@@ -223,6 +223,59 @@ int gm_split_rhat_ess_dist(gm_comm* comm, const void* dev_sample, gm_dtype dtype
                            int64_t stride_chain, int64_t stride_draw, int64_t stride_param,
                            float* rhat_out, float* ess_out);
 
+/* ---- granular BatchVector ops (tier 2 of the boundary) ----------------
+ * The reference's plug-in seam is the BatchVector trait implemented for
+ * Tensor<B,2> [n_chains, dim] (euclidean.rs:145-195, 358-534) plus
+ * BatchedHamiltonianTarget::logp_and_grad (batched_hmc.rs:18-22). These
+ * entry points are those operations on caller-held DEVICE buffers, so a
+ * BatchVector implementation (or BatchedGenericHMC::step itself,
+ * batched_hmc.rs:129-190) can be driven op by op. A step composed of them
+ * equals the fused gm_step bit for bit: same Philox streams (momentum:
+ * tag 2, accept: tag 3, keyed by global chain id and step), same rounding,
+ * and per-chain sums in the canonical order of the default layout of `dim`.
+ * Matrices are [n_chains][dim] row-major, energies [n_chains], masks
+ * uint8 [n_chains]. Ops are enqueued in order on the device's null stream;
+ * gm_device_synchronize waits for them. */
+int gm_malloc(void** dev_ptr, size_t bytes);
+int gm_free(void* dev_ptr);
+int gm_memcpy_htod(void* dev_dst, const void* host_src, size_t bytes);
+int gm_memcpy_dtoh(void* host_dst, const void* dev_src, size_t bytes);
+/* assign (euclidean.rs:380-382): dev_dst = dev_src */
+int gm_memcpy_dtod(void* dev_dst, const void* dev_src, size_t bytes);
+
+/* kinetic_energy (euclidean.rs:464-472): ke[c] = (sum_j p[c,j]^2) * 0.5 */
+int gm_bv_kinetic_energy(gm_dtype dtype, int64_t n_chains, int64_t dim, const void* p, void* ke);
+/* masked_assign (euclidean.rs:474-482): x[c,:] = other[c,:] where mask[c] != 0 */
+int gm_bv_masked_assign(gm_dtype dtype, int64_t n_chains, int64_t dim, void* x, const void* other,
+                        const uint8_t* mask);
+/* add_scaled_assign (euclidean.rs:392-394): x = x + other * alpha, two
+ * roundings, alpha rounded to dtype first; n = number of elements */
+int gm_bv_add_scaled_assign(gm_dtype dtype, int64_t n, void* x, const void* other, double alpha);
+/* fill_random_normal (euclidean.rs:484-496): out[c,j] = momentum draw of
+ * chain chain_offset+c, coordinate j, transition `step` under `seed` */
+int gm_bv_fill_random_normal(gm_dtype dtype, int64_t n_chains, int64_t dim, void* out, uint64_t seed,
+                             uint32_t chain_offset, uint64_t step);
+/* sample_uniform (euclidean.rs:498-509): out[c] in [0,1), the accept draw */
+int gm_bv_sample_uniform(gm_dtype dtype, int64_t n_chains, void* out, uint64_t seed,
+                         uint32_t chain_offset, uint64_t step);
+/* energy_sub / energy_add / energy_neg / energy_ln (euclidean.rs:511-525) */
+int gm_bv_energy_sub(gm_dtype dtype, int64_t n, const void* a, const void* b, void* out);
+int gm_bv_energy_add(gm_dtype dtype, int64_t n, const void* a, const void* b, void* out);
+int gm_bv_energy_neg(gm_dtype dtype, int64_t n, const void* a, void* out);
+int gm_bv_energy_ln(gm_dtype dtype, int64_t n, const void* a, void* out);
+/* accept_mask (euclidean.rs:527-533): mask[c] = log_accept[c] >= ln_u[c]
+ * (NaN -> 0) */
+int gm_bv_accept_mask(gm_dtype dtype, int64_t n, const void* log_accept, const void* ln_u,
+                      uint8_t* mask);
+
+/* A built-in target resident on the device, for logp_and_grad on device
+ * buffers (BatchedHamiltonianTarget, batched_hmc.rs:18-22; hmc.rs:42-61). */
+typedef struct gm_bv_target gm_bv_target;
+int gm_bv_target_create(const gm_target* target, gm_dtype dtype, gm_bv_target** out);
+/* grad[c,:] = d logp / d x at x[c,:]; returns logp[c] (either output may be NULL) */
+int gm_bv_logp_and_grad(gm_bv_target* t, int64_t n_chains, const void* x, void* grad, void* logp);
+int gm_bv_target_destroy(gm_bv_target* t);
+
 #ifdef __cplusplus
 }
 #endif

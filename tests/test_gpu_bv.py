@@ -1,0 +1,120 @@
+"""Tier-2 boundary: the granular BatchVector ops (gm_bv_*, euclidean.rs:447-534)
+on device buffers. Each op is checked against the oracle / IEEE arithmetic,
+and the reference's own step loop (BatchedGenericHMC::step,
+batched_hmc.rs:129-190) composed from them must reproduce the fused kernel
+bit for bit."""
+import numpy as np
+import pytest
+
+from tests._oracle import Target
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def bv(gm):
+    return gm.batch_vector
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_elementwise_ops_ieee(bv, dtype):
+    rng = np.random.default_rng(3)
+    C, D = 37, 11
+    x = rng.standard_normal((C, D)).astype(dtype)
+    o = rng.standard_normal((C, D)).astype(dtype)
+    dx, do = bv.DeviceMatrix.from_host(x), bv.DeviceMatrix.from_host(o)
+    alpha = dtype(0.5) * dtype(0.013)
+    bv.add_scaled_assign(dx, do, alpha)
+    np.testing.assert_array_equal(dx.to_host(), x + o * alpha)  # two roundings (euclidean.rs:392-394)
+    mask = (rng.random(C) < 0.5).astype(np.uint8)
+    y = dx.to_host()
+    bv.masked_assign(dx, do, bv.DeviceMatrix.from_host(mask))
+    np.testing.assert_array_equal(dx.to_host(), np.where(mask[:, None] == 1, o, y))
+    a = rng.standard_normal(C).astype(dtype)
+    b = rng.standard_normal(C).astype(dtype)
+    da, db = bv.DeviceMatrix.from_host(a), bv.DeviceMatrix.from_host(b)
+    np.testing.assert_array_equal(bv.energy_sub(da, db).to_host(), a - b)
+    np.testing.assert_array_equal(bv.energy_add(da, db).to_host(), a + b)
+    np.testing.assert_array_equal(bv.energy_neg(da).to_host(), -a)
+    la = np.array([0.0, -1.0, np.nan, 2.0, -np.inf], dtype=dtype)
+    lu = np.array([0.0, -0.5, -1.0, np.nan, -np.inf], dtype=dtype)
+    m = bv.accept_mask(bv.DeviceMatrix.from_host(la), bv.DeviceMatrix.from_host(lu)).to_host()
+    np.testing.assert_array_equal(m, [1, 0, 0, 0, 1])  # >=, NaN rejects (euclidean.rs:532)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_random_fills_and_ln_match_oracle(bv, oracle, dtype):
+    C, D, seed, step, off = 9, 5, 77, 13, 100
+    z = bv.DeviceMatrix((C, D), dtype)
+    bv.fill_random_normal(z, seed, step, chain_offset=off)
+    sfx = "f" if dtype == np.float32 else "d"
+    nrm = getattr(oracle.lib, f"or_normal_{sfx}")
+    exp = np.array([[nrm(seed, off + c, step, 2, j) for j in range(D)] for c in range(C)], dtype=dtype)
+    np.testing.assert_array_equal(z.to_host(), exp)
+    u = bv.sample_uniform(C, dtype, seed, step, chain_offset=off)
+    uni = getattr(oracle.lib, f"or_uniform_co_{sfx}")
+    ue = np.array([uni(seed, off + c, step, 3, 0) for c in range(C)], dtype=dtype)
+    np.testing.assert_array_equal(u.to_host(), ue)
+    lg = getattr(oracle.lib, f"or_log_{sfx}")
+    np.testing.assert_array_equal(bv.energy_ln(u).to_host(), np.array([lg(v) for v in ue], dtype=dtype))
+
+
+@pytest.mark.parametrize("D", [1, 7, 64, 100, 300])
+def test_kinetic_energy_canonical_order(gm, bv, oracle, D):
+    """K(p) = (sum p^2)*0.5 equals -logp of IsotropicGaussian(1) in the same
+    canonical summation order (scaling by 0.5 and dividing by 1 are exact)."""
+    rng = np.random.default_rng(D)
+    p = rng.standard_normal((17, D)).astype(np.float32)
+    ke = bv.kinetic_energy(bv.DeviceMatrix.from_host(p)).to_host()
+    s = gm.HMC(gm.IsotropicGaussian(1.0), p, 0.1, 1)
+    lanes, elems = s.layout()
+    lp, _ = oracle.logp_grad(Target(2, D, std=1.0), p, lanes, elems, np.float32)
+    np.testing.assert_array_equal(ke, -lp)
+
+
+def test_logp_and_grad_device(gm, bv, oracle):
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((33, 64)).astype(np.float32)
+    t = bv.BatchTarget(gm.RosenbrockND(), 64, np.float32)
+    dx = bv.DeviceMatrix.from_host(x)
+    g = bv.DeviceMatrix.like(dx)
+    lp = t.logp_and_grad(dx, g).to_host()
+    elp, eg = oracle.logp_grad(Target(1, 64), x, 64, 1, np.float32)
+    np.testing.assert_array_equal(lp, elp)
+    np.testing.assert_array_equal(g.to_host(), eg)
+
+
+CASES = [
+    ("rosen64_f32", lambda gm: gm.RosenbrockND(), 64, np.float32, 0.01, 7),
+    ("rosen10_f64", lambda gm: gm.RosenbrockND(), 10, np.float64, 0.02, 5),
+    ("rosen100_f32", lambda gm: gm.RosenbrockND(), 100, np.float32, 0.005, 4),
+    ("iso7_f32", lambda gm: gm.IsotropicGaussian(1.5), 7, np.float32, 0.3, 6),
+    ("gauss2d_f64", lambda gm: gm.DiffableGaussian2D([0.0, 1.0], [[4.0, 2.0], [2.0, 3.0]]), 2,
+     np.float64, 0.1, 10),
+]
+
+
+@pytest.mark.parametrize("name,mk,D,dtype,eps,L", CASES, ids=[c[0] for c in CASES])
+def test_composed_step_equals_fused_kernel(gm, bv, name, mk, D, dtype, eps, L):
+    """batched_hmc.rs:129-190 op by op == the fused kernel, bitwise, including
+    a chain offset (sharded streams) and a mid-block start (step 3)."""
+    C, off = 48, 1000
+    x0 = gm.init_with_seed(C, D, 11, dtype)
+    composed = bv.BatchedGenericHMC(mk(gm), x0, eps, L, seed=9, chain_offset=off)
+    fused = gm.HMC(mk(gm), x0, eps, L, dtype=dtype, chain_offset=off).set_seed(9)
+    a = composed.run(3, 0)
+    b = fused.run(3, 0)
+    np.testing.assert_array_equal(a, b)
+    a = composed.run(4, 2)
+    b = fused.run(4, 2)
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(composed.positions(), fused.positions())
+
+
+def test_bv_rejects_bad_arguments(gm, bv):
+    a = bv.DeviceMatrix((4, 3), np.float32)
+    b = bv.DeviceMatrix((4, 2), np.float32)
+    with pytest.raises(ValueError):
+        bv.add_scaled_assign(a, b, 1.0)
+    lib = gm._lib.load()
+    assert lib.gm_bv_kinetic_energy(7, 4, 3, None, None) == gm._lib.GM_EINVAL  # bad dtype
