@@ -13,11 +13,12 @@ from .distributions import (DenseGaussian, DiffableGaussian2D, Gaussian2D, Isotr
 from .hmc import HMC
 from .metropolis_hastings import MetropolisHastings
 from .nuts import NUTS, NUTSChain
-from .stats import BasicStats, RunStats, basic_stats, split_rhat_mean_ess
+from .stats import (BasicStats, ChainStats, MultiChainTracker, Progress, RunStats, basic_stats,
+                    split_rhat_mean_ess)
 
 __all__ = [
     "HMC", "NUTS", "NUTSChain", "MetropolisHastings", "RosenbrockND", "Rosenbrock2D",
     "IsotropicGaussian", "DiffableGaussian2D", "DenseGaussian", "Gaussian2D", "init", "init_det",
     "init_with_seed", "split_rhat_mean_ess", "basic_stats", "BasicStats", "RunStats", "GMError",
-    "batch_vector",
+    "batch_vector", "MultiChainTracker", "ChainStats", "Progress",
 ]

@@ -41,6 +41,13 @@ class gm_target(C.Structure):
     ]
 
 
+class gm_progress(C.Structure):
+    _fields_ = [("done", C.c_int64), ("total", C.c_int64), ("p_accept", C.c_float),
+                ("max_rhat", C.c_float)]
+
+
+PROGRESS_FN = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(gm_progress))
+
 _vp = C.c_void_p
 _i64 = C.c_int64
 _i32 = C.c_int32
@@ -84,6 +91,13 @@ SIGNATURES = {
     "gm_comm_init": (_ip, [_vp, _i32, _i32, C.POINTER(_vp)]),
     "gm_comm_destroy": (_ip, [_vp]),
     "gm_split_rhat_ess_dist": (_ip, [_vp, _vp, _ip, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
+    # run_progress statistics
+    "gm_run_progress_cb": (_ip, [_vp, _i64, _i64, _vp, _vp, _vp, PROGRESS_FN, _vp, _dbl]),
+    "gm_sampler_chain_stats": (_ip, [_vp, C.POINTER(_u64), _vp, _vp, _vp]),
+    "gm_mct_create": (_ip, [_i64, _i64, C.POINTER(_vp)]),
+    "gm_mct_step": (_ip, [_vp, _vp, _ip]),
+    "gm_mct_stats": (_ip, [_vp, _vp, _vp, _vp]),
+    "gm_mct_destroy": (_ip, [_vp]),
     # granular BatchVector ops (tier 2)
     "gm_malloc": (_ip, [C.POINTER(_vp), C.c_size_t]),
     "gm_free": (_ip, [_vp]),

@@ -7,7 +7,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from .stats import RunStats, split_rhat_mean_ess_device
+from .stats import ChainStats, Progress, RunStats, _print_progress, split_rhat_mean_ess_device
 
 
 @dataclass
@@ -89,18 +89,50 @@ class Sampler:
         _lib.check(self._lib.gm_run_device(self._h, n_collect, n_discard, C.byref(p)))
         return DeviceSamples(p.value or 0, n_collect, self.n_chains, self.dim, self.dtype, self)
 
-    def run_progress(self, n_collect: int, n_discard: int):
+    _progress_prefix = "Sampler"
+    _progress_interval = 1.0
+
+    def run_progress(self, n_collect: int, n_discard: int, progress=None, interval: float | None = None):
         """(sample [n_chains, n_collect, dim], RunStats | None): the statistics
-        are the device-side split-R-hat/ESS of the collected draws."""
+        are the device-side split-R-hat/ESS of the collected draws.
+
+        `progress`: None (silent), True (a progress line on stderr, as the
+        reference's progress bars, hmc.rs:255-288 / core.rs:272-345), or a
+        callable receiving a `Progress` (done, total, p_accept, max_rhat)
+        from the device-side trackers at most every `interval` seconds and
+        after the last transition."""
         out = np.empty((self.n_chains, n_collect, self.dim), dtype=self.dtype)
+        cb = _lib.PROGRESS_FN()
+        if progress is not None and progress is not False:
+            fn = _print_progress(self._progress_prefix) if progress is True else progress
+
+            def _cb(_user, info):
+                i = info.contents
+                fn(Progress(int(i.done), int(i.total), float(i.p_accept), float(i.max_rhat)))
+            cb = _lib.PROGRESS_FN(_cb)
+        iv = self._progress_interval if interval is None else float(interval)
+        stats = None
         if n_collect >= 2:
             rhat = np.empty(self.dim, dtype=np.float32)
             ess = np.empty(self.dim, dtype=np.float32)
-            _lib.check(self._lib.gm_run_progress(self._h, n_collect, n_discard, _lib.ptr(out),
-                                                 _lib.ptr(rhat), _lib.ptr(ess)))
-            return out, RunStats.from_arrays(rhat, ess)
-        _lib.check(self._lib.gm_run_progress(self._h, n_collect, n_discard, _lib.ptr(out), None, None))
-        return out, None
+            _lib.check(self._lib.gm_run_progress_cb(self._h, n_collect, n_discard, _lib.ptr(out),
+                                                    _lib.ptr(rhat), _lib.ptr(ess), cb, None, iv))
+            stats = RunStats.from_arrays(rhat, ess)
+        else:
+            _lib.check(self._lib.gm_run_progress_cb(self._h, n_collect, n_discard, _lib.ptr(out), None,
+                                                    None, cb, None, iv))
+        return out, stats
+
+    def chain_stats(self) -> "ChainStats":
+        """ChainTracker::stats of every chain after an MH / NUTS run_progress
+        (stats.rs:122-131): n, p_accept [C], mean [C, dim], sm2 [C, dim]."""
+        n = C.c_uint64()
+        p = np.empty(self.n_chains, dtype=np.float32)
+        m = np.empty((self.n_chains, self.dim), dtype=np.float32)
+        v = np.empty((self.n_chains, self.dim), dtype=np.float32)
+        _lib.check(self._lib.gm_sampler_chain_stats(self._h, C.byref(n), _lib.ptr(p), _lib.ptr(m),
+                                                    _lib.ptr(v)))
+        return ChainStats(int(n.value), p, m, v)
 
     def copy_samples(self, n_collect: int) -> np.ndarray:
         """Samples of the last run, [n_chains, n_collect, dim] on the host."""

@@ -49,6 +49,30 @@ struct HmcLaunch {
 hipError_t launch_hmc(gm_dtype dt, const TargetDev& tg, const Layout& lay, const HmcLaunch& a,
                       hipStream_t st);
 
+// ---- run_progress statistics (gm_track.h, tracker_kernels.hip) -------------
+// Per-chain ChainTracker state (stats.rs:24-131), f32 [C][D] and [C]; mean
+// is null when tracking is off. n0 = tracker steps before this launch.
+struct TrackLaunch {
+  float* mean = nullptr;
+  float* msq = nullptr;
+  float* last = nullptr;
+  float* p = nullptr;
+  unsigned long long n0 = 0;
+};
+// ChainTracker::new for every chain from the current positions
+hipError_t launch_ct_init(gm_dtype dt, long long C, int D, const void* q, const TrackLaunch& t,
+                          hipStream_t st);
+// ChainTracker::stats of every chain + collect_rhat (stats.rs:122-193) -> rhat[D],
+// and the mean acceptance EMA over chains -> p_mean[0]
+hipError_t launch_ct_rhat(long long C, int D, unsigned long long n, const TrackLaunch& t, float* rhat,
+                          float* p_mean, hipStream_t st);
+// MultiChainTracker::step / rhat (stats.rs:199-339) on [C][P] positions
+hipError_t launch_mct_step(gm_dtype dt, long long C, int P, const void* x, float* mean, float* msq,
+                           float* last, int* flags, float* p_accept, unsigned long long n_after,
+                           hipStream_t st);
+hipError_t launch_mct_rhat(long long C, int P, unsigned long long n, const float* mean, const float* msq,
+                           float* rhat, hipStream_t st);
+
 // ---- MH --------------------------------------------------------------------
 struct MhLaunch {
   void* q = nullptr;
@@ -64,6 +88,7 @@ struct MhLaunch {
   int n_steps = 0;
   int collect_from = 0;
   long long sample_row0 = 0;
+  TrackLaunch trk;              // run_progress chain trackers (off when trk.mean is null)
 };
 hipError_t launch_mh(gm_dtype dt, const TargetDev& tg, const Layout& lay, const MhLaunch& a,
                      hipStream_t st);

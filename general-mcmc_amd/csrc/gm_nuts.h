@@ -1,5 +1,6 @@
 // gm_nuts.h — host-side interface of the NUTS engine (nuts_kernels.hip).
 #pragma once
+#include <functional>
 #include <vector>
 
 #include "gm_internal.h"
@@ -28,12 +29,16 @@ struct NutsState {
 
 int nuts_init_state(NutsState* ns, gm_dtype dt, long long C, int D, int max_depth);
 void nuts_free_state(NutsState* ns);
+// Called after each launch with the transitions done so far in the run (the
+// launch may still be in flight); non-zero aborts the run with that status.
+using StepHook = std::function<int(long long)>;
 // progress = 0: NUTS::run semantics; 1: run_progress semantics (see gmcmc.h)
 int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay, void* q,
              long long* accepts, void* samples, long long C, int D, double target_accept,
              uint64_t seed, uint64_t* step, uint32_t chain_offset, long long total,
              long long n_discard, int progress, long long steps_per_launch, hipStream_t st,
-             std::vector<hipEvent_t>& evs, double* ms, long long* launches);
+             std::vector<hipEvent_t>& evs, double* ms, long long* launches,
+             const TrackLaunch* trk = nullptr, const StepHook* hook = nullptr);
 int nuts_get_step_size(NutsState& ns, gm_dtype dt, long long C, double* eps, double* eps_bar);
 int nuts_get_leapfrogs(NutsState& ns, long long C, long long* out);
 

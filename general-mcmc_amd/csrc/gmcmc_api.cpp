@@ -9,6 +9,7 @@
 // inside one launch with the chain state resident in registers.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -118,6 +119,39 @@ struct gm_sampler {
   long long total_steps = 0;  // transitions since creation
   long long last_rows = 0;    // sample rows produced by the last run
   NutsState nuts;
+  // run_progress statistics: per-chain trackers (MH, NUTS) and a
+  // MultiChainTracker (HMC), one allocation each (TrackSet)
+  void* d_trk = nullptr;
+  size_t trk_bytes = 0;
+  unsigned long long trk_n = 0;  // ChainTracker steps taken (0: no stats yet)
+  void* d_mct = nullptr;
+  size_t mct_bytes = 0;
+};
+
+// Views into one tracker allocation: mean, msq, last [C*D]; p [C]; flags [C]
+// (int); rhat [D]; scalar [1].
+struct TrackSet {
+  float *mean, *msq, *last, *p, *rhat, *scalar;
+  int* flags;
+  static size_t bytes(long long C, int D) { return sizeof(float) * (3 * (size_t)C * D + 2 * C + D + 1); }
+  TrackSet(void* base, long long C, int D) {
+    float* f = (float*)base;
+    mean = f;
+    msq = f + (size_t)C * D;
+    last = f + 2 * (size_t)C * D;
+    p = f + 3 * (size_t)C * D;
+    flags = (int*)(p + C);
+    rhat = (float*)(flags + C);
+    scalar = rhat + D;
+  }
+  TrackLaunch launch() const {
+    TrackLaunch t;
+    t.mean = mean;
+    t.msq = msq;
+    t.last = last;
+    t.p = p;
+    return t;
+  }
 };
 
 static int ensure_buf(void** p, size_t* cap, size_t need) {
@@ -450,7 +484,9 @@ static int hmc_lf_unroll(long long waves) {
   return waves <= simds ? 4 : 1;
 }
 
-static int run_steps(gm_sampler* s, long long total, long long collect_from, int progress) {
+static int run_steps(gm_sampler* s, long long total, long long collect_from, int progress,
+                     const TrackLaunch* trk = nullptr, const StepHook* hook = nullptr,
+                     long long chunk_override = 0) {
   GM_HIP(hipSetDevice(s->device));
   s->last_ms = 0;
   s->last_launches = 0;
@@ -459,11 +495,11 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
   if (s->kind == K_NUTS) {
     int rc = nuts_run(s->nuts, s->dt, s->tg, s->lay, s->d_q, s->d_acc, s->d_samples, s->C, s->D,
                       s->target_accept, s->seed, &s->step, s->chain_offset, total, collect_from,
-                      progress, s->steps_per_launch, s->stream, s->evs, &s->last_ms,
-                      &s->last_launches);
+                      progress, chunk_override > 0 ? chunk_override : s->steps_per_launch,
+                      s->stream, s->evs, &s->last_ms, &s->last_launches, trk, hook);
     return rc;
   }
-  const long long chunk = s->steps_per_launch;
+  const long long chunk = chunk_override > 0 ? chunk_override : s->steps_per_launch;
   const long long n_launch = (total + chunk - 1) / chunk;
   while ((long long)s->evs.size() < 2 * n_launch) {
     hipEvent_t ev;
@@ -513,6 +549,10 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
       a.n_steps = (int)n;
       a.collect_from = (int)cf;
       a.sample_row0 = row0;
+      if (trk) {
+        a.trk = *trk;
+        a.trk.n0 = trk->n0 + (unsigned long long)start;
+      }
       e = launch_mh(s->dt, s->tg, s->lay, a, s->stream);
     }
     if (e != hipSuccess) {
@@ -520,6 +560,10 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
       return GM_EHIP;
     }
     GM_HIP(hipEventRecord(s->evs[2 * li + 1], s->stream));
+    if (hook && *hook) {
+      const int rc = (*hook)(start + n);
+      if (rc) return rc;
+    }
   }
   s->step += total;
   s->total_steps += total;
@@ -594,10 +638,106 @@ int gm_run(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out) {
   return gm_copy_samples(s, out);
 }
 
-int gm_run_progress(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out,
-                    float* rhat_out, float* ess_out) {
-  int rc = run_impl(s, n_collect, n_discard, 1);
+static float max_skipnan(const float* v, long long n) {  // stats.rs:154-161
+  float m = NAN;
+  bool any = false;
+  for (long long i = 0; i < n; ++i)
+    if (!std::isnan(v[i])) {
+      m = any ? std::fmax(m, v[i]) : v[i];
+      any = true;
+    }
+  return m;
+}
+
+int gm_run_progress_cb(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out,
+                       float* rhat_out, float* ess_out, gm_progress_fn cb, void* user,
+                       double interval_s) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(n_collect >= 0 && n_discard >= 0, "n_collect and n_discard must be >= 0");
+  GM_HIP(hipSetDevice(s->device));
+  s->last_rows = n_collect;
+  int rc = ensure_buf(&s->d_samples, &s->samples_bytes, (size_t)n_collect * s->C * s->D * s->esz);
   if (rc) return rc;
+  const long long C = s->C, total = n_collect + n_discard;
+  const int D = s->D;
+  using clk = std::chrono::steady_clock;
+  auto t_last = clk::now();
+  auto due = [&](bool last) {
+    return last || std::chrono::duration<double>(clk::now() - t_last).count() >= interval_s;
+  };
+  // with a callback, launches are cut so that it can fire between them
+  long long chunk = 0;
+  if (cb) {
+    chunk = total / 32 > 0 ? total / 32 : 1;
+    if (chunk > s->steps_per_launch) chunk = s->steps_per_launch;
+  }
+  std::vector<float> rh(D);
+  gm_progress info{};
+  if (s->kind == K_HMC) {
+    // burn-in, then the collection with a MultiChainTracker stepped on the
+    // current positions at each sync point (hmc.rs:252-290)
+    if (n_discard > 0) {
+      rc = run_steps(s, n_discard, n_discard, 1);
+      if (rc) return rc;
+    }
+    StepHook hook;
+    unsigned long long mct_n = 0;
+    if (cb) {
+      rc = ensure_buf(&s->d_mct, &s->mct_bytes, TrackSet::bytes(C, D));
+      if (rc) return rc;
+      GM_HIP(hipMemsetAsync(s->d_mct, 0, TrackSet::bytes(C, D), s->stream));  // new(): zeros, p 0
+      hook = [&](long long done) -> int {
+        const bool last = done >= n_collect;
+        if (!due(last)) return GM_OK;
+        TrackSet ts(s->d_mct, C, D);
+        ++mct_n;
+        GM_HIP(launch_mct_step(s->dt, C, D, s->d_q, ts.mean, ts.msq, ts.last, ts.flags, ts.p, mct_n,
+                               s->stream));
+        GM_HIP(launch_mct_rhat(C, D, mct_n, ts.mean, ts.msq, ts.rhat, s->stream));
+        float p = 0;
+        GM_HIP(hipMemcpyAsync(rh.data(), ts.rhat, sizeof(float) * D, hipMemcpyDeviceToHost, s->stream));
+        GM_HIP(hipMemcpyAsync(&p, ts.p, sizeof(float), hipMemcpyDeviceToHost, s->stream));
+        GM_HIP(hipStreamSynchronize(s->stream));
+        info.done = done;
+        info.total = n_collect;
+        info.p_accept = p;
+        info.max_rhat = max_skipnan(rh.data(), D);
+        cb(user, &info);
+        t_last = clk::now();
+        return GM_OK;
+      };
+    }
+    rc = run_steps(s, n_collect, 0, 1, nullptr, cb ? &hook : nullptr, chunk);
+    if (rc) return rc;
+  } else {
+    // MH (core.rs:132-176) and NUTS (generic_nuts.rs:675-716): every chain's
+    // ChainTracker steps after every transition, burn-in included
+    rc = ensure_buf(&s->d_trk, &s->trk_bytes, TrackSet::bytes(C, D));
+    if (rc) return rc;
+    TrackSet ts(s->d_trk, C, D);
+    TrackLaunch tl = ts.launch();
+    GM_HIP(launch_ct_init(s->dt, C, D, s->d_q, tl, s->stream));
+    s->trk_n = 0;
+    StepHook hook = [&](long long done) -> int {
+      const bool last = done >= total;
+      if (!due(last)) return GM_OK;
+      float pm = 0;
+      GM_HIP(launch_ct_rhat(C, D, (unsigned long long)done, tl, ts.rhat, ts.scalar, s->stream));
+      GM_HIP(hipMemcpyAsync(rh.data(), ts.rhat, sizeof(float) * D, hipMemcpyDeviceToHost, s->stream));
+      GM_HIP(hipMemcpyAsync(&pm, ts.scalar, sizeof(float), hipMemcpyDeviceToHost, s->stream));
+      GM_HIP(hipStreamSynchronize(s->stream));
+      info.done = done;
+      info.total = total;
+      info.p_accept = pm;
+      info.max_rhat = C >= 2 ? max_skipnan(rh.data(), D) : NAN;  // core.rs:321 (>= 2 chains)
+      cb(user, &info);
+      t_last = clk::now();
+      return GM_OK;
+    };
+    rc = run_steps(s, total, n_discard, 1, &tl, cb ? &hook : nullptr, chunk);
+    if (rc) return rc;
+    s->trk_n = (unsigned long long)total;
+  }
   if (out && n_collect > 0) {
     rc = gm_copy_samples(s, out);
     if (rc) return rc;
@@ -610,6 +750,35 @@ int gm_run_progress(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* o
     if (rc) return rc;
     if (rhat_out) memcpy(rhat_out, r.data(), sizeof(float) * s->D);
     if (ess_out) memcpy(ess_out, e.data(), sizeof(float) * s->D);
+  }
+  return GM_OK;
+}
+
+int gm_run_progress(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out,
+                    float* rhat_out, float* ess_out) {
+  return gm_run_progress_cb(s, n_collect, n_discard, out, rhat_out, ess_out, nullptr, nullptr, 0.0);
+}
+
+int gm_sampler_chain_stats(gm_sampler* s, uint64_t* n, float* p_accept, float* mean, float* sm2) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(s->kind != K_HMC, "chain trackers are kept by the MH and NUTS run_progress");
+  GM_REQ(s->d_trk != nullptr, "no run_progress has been run");
+  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  const long long C = s->C;
+  const int D = s->D;
+  TrackSet ts(s->d_trk, C, D);
+  if (n) *n = s->trk_n;
+  if (p_accept) GM_HIP(hipMemcpy(p_accept, ts.p, sizeof(float) * C, hipMemcpyDeviceToHost));
+  if (mean || sm2) {
+    std::vector<float> m((size_t)C * D), q((size_t)C * D);
+    GM_HIP(hipMemcpy(m.data(), ts.mean, sizeof(float) * C * D, hipMemcpyDeviceToHost));
+    GM_HIP(hipMemcpy(q.data(), ts.msq, sizeof(float) * C * D, hipMemcpyDeviceToHost));
+    if (mean) memcpy(mean, m.data(), sizeof(float) * C * D);
+    if (sm2) {  // ChainTracker::stats (stats.rs:122-131)
+      const float nf = (float)s->trk_n;
+      for (long long i = 0; i < C * D; ++i) sm2[i] = (q[i] - m[i] * m[i]) * nf / (nf - 1.0f);
+    }
   }
   return GM_OK;
 }
@@ -660,6 +829,71 @@ int gm_nuts_get_step_size(gm_sampler* s, double* eps, double* eps_bar) {
   return nuts_get_step_size(s->nuts, s->dt, s->C, eps, eps_bar);
 }
 
+struct gm_mct {
+  long long C = 0;
+  int P = 0;
+  int device = 0;
+  unsigned long long n = 0;
+  void* buf = nullptr;
+};
+
+int gm_mct_create(int64_t n_chains, int64_t n_params, gm_mct** out) {
+  GM_REQ(out, "out is NULL");
+  *out = nullptr;
+  GM_REQ(n_chains >= 1 && n_params >= 1 && n_params <= (1 << 30), "bad tracker shape");
+  gm_mct* t = new gm_mct();
+  t->C = n_chains;
+  t->P = (int)n_params;
+  hipGetDevice(&t->device);
+  size_t cap = 0;
+  int rc = ensure_buf(&t->buf, &cap, TrackSet::bytes(t->C, t->P));
+  if (rc) {
+    delete t;
+    return rc;
+  }
+  GM_HIP(hipMemset(t->buf, 0, TrackSet::bytes(t->C, t->P)));
+  *out = t;
+  return GM_OK;
+}
+
+int gm_mct_step(gm_mct* t, const void* x, gm_dtype dt) {
+  GM_REQ(t && x, "bad arguments");
+  GM_REQ(dt == GM_F32 || dt == GM_F64, "bad dtype");
+  GM_HIP(hipSetDevice(t->device));
+  TrackSet ts(t->buf, t->C, t->P);
+  ++t->n;
+  GM_HIP(launch_mct_step(dt, t->C, t->P, x, ts.mean, ts.msq, ts.last, ts.flags, ts.p, t->n, nullptr));
+  return GM_OK;
+}
+
+int gm_mct_stats(gm_mct* t, float* p_accept, float* rhat, float* max_rhat) {
+  GM_REQ(t, "tracker is NULL");
+  GM_HIP(hipSetDevice(t->device));
+  TrackSet ts(t->buf, t->C, t->P);
+  if (p_accept) GM_HIP(hipMemcpy(p_accept, ts.p, sizeof(float), hipMemcpyDeviceToHost));
+  if (rhat || max_rhat) {
+    GM_HIP(launch_mct_rhat(t->C, t->P, t->n, ts.mean, ts.msq, ts.rhat, nullptr));
+    std::vector<float> r(t->P);
+    GM_HIP(hipMemcpy(r.data(), ts.rhat, sizeof(float) * t->P, hipMemcpyDeviceToHost));
+    if (rhat) memcpy(rhat, r.data(), sizeof(float) * t->P);
+    if (max_rhat) {  // MultiChainTracker::max_rhat: reduce(f32::max) (stats.rs:298-305)
+      float m = r[0];
+      for (int i = 1; i < t->P; ++i) m = std::fmax(m, r[i]);
+      *max_rhat = m;
+    }
+  }
+  return GM_OK;
+}
+
+int gm_mct_destroy(gm_mct* t) {
+  if (!t) return GM_OK;
+  hipSetDevice(t->device);
+  hipDeviceSynchronize();
+  if (t->buf) hipFree(t->buf);
+  delete t;
+  return GM_OK;
+}
+
 int gm_destroy(gm_sampler* s) {
   if (!s) return GM_OK;
   hipSetDevice(s->device);
@@ -672,6 +906,8 @@ int gm_destroy(gm_sampler* s) {
   if (s->d_acc) hipFree(s->d_acc);
   if (s->d_samples) hipFree(s->d_samples);
   if (s->d_tmp) hipFree(s->d_tmp);
+  if (s->d_trk) hipFree(s->d_trk);
+  if (s->d_mct) hipFree(s->d_mct);
   nuts_free_state(&s->nuts);
   if (s->stream) hipStreamDestroy(s->stream);
   delete s;

@@ -11,6 +11,7 @@
 // The current log-density is carried across steps (the reference recomputes
 // it, :308 -- same value).
 #include "gm_layouts.h"
+#include "gm_track.h"
 
 namespace gm {
 
@@ -43,6 +44,9 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   long long acc = 0;
   NormalCache<T> ncache[E];
   UniformCache<T> ucache;
+  const bool track = a.trk.mean != nullptr;  // run_progress (core.rs:146-163)
+  ChainTrack<LPC, E> tr;
+  if (track) tr.load(a.trk, c, lane, D);
   for (int s = 0; s < a.n_steps; ++s) {
     const uint64_t st = a.step0 + (uint64_t)s;
     T qpart = (T)0;
@@ -69,6 +73,7 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
       lp = lp1;
       ++acc;
     }
+    if (track) tr.step(x, a.trk.n0 + (unsigned long long)s + 1ull, lane, D);
     if (s >= a.collect_from) {
       T* __restrict__ out = (T*)a.samples + ((a.sample_row0 + (s - a.collect_from)) * a.C + c) * D;
 #pragma unroll
@@ -83,6 +88,7 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
     const int i = lane * E + e;
     if (i < D) qs[c * D + i] = x[e];
   }
+  if (track) tr.store(a.trk, c, lane, D);
   if (lane == 0) {
     ((T*)a.logp)[c] = lp;
     a.accepts[c] += acc;

@@ -23,6 +23,7 @@
 // ever reads back what it wrote itself, so no cross-lane ordering is needed.
 #include "gm_layouts.h"
 #include "gm_nuts.h"
+#include "gm_track.h"
 
 namespace gm {
 
@@ -54,6 +55,7 @@ struct NutsLaunch {
   long long t0 = 0;          // transitions already done in this run before this launch
   long long row_shift = 0;   // state after t transitions goes to row t - row_shift
   long long n_rows = 0;
+  TrackLaunch trk;           // run_progress chain trackers (off when trk.mean is null)
 };
 
 template <int LPC, int E, class T>
@@ -209,6 +211,9 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
 
   long long acc = 0, nlf = 0;
   NormalCache<T> ncache[E];
+  const bool track = a.trk.mean != nullptr;  // run_progress (generic_nuts.rs:688-704)
+  ChainTrack<LPC, E> tr;
+  if (track) tr.load(a.trk, c, lane, D);
   for (int s = 0; s < a.n_steps; ++s) {
     const uint64_t st = a.step0 + (uint64_t)s;
     const long long m = a.m0 + s + 1;
@@ -347,8 +352,10 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     } else {
       eps = eps_bar;
     }
+    if (track) tr.step(q, a.trk.n0 + (unsigned long long)s + 1ull, lane, D);
     record(a.t0 + s + 1);
   }
+  if (track) tr.store(a.trk, c, lane, D);
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int i = lane * E + e;
@@ -427,7 +434,8 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
              long long* accepts, void* samples, long long C, int D, double target_accept,
              uint64_t seed, uint64_t* step, uint32_t chain_offset, long long total,
              long long n_discard, int progress, long long steps_per_launch, hipStream_t st,
-             std::vector<hipEvent_t>& evs, double* ms, long long* launches) {
+             std::vector<hipEvent_t>& evs, double* ms, long long* launches, const TrackLaunch* trk,
+             const StepHook* hook) {
   const size_t esz = dt == GM_F32 ? 4 : 8;
   // scalar stack is per lane; (re)size for the current layout
   const long long lanes_total = C * lay.lanes;
@@ -495,6 +503,10 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     a.t0 = start;
     a.row_shift = row_shift;
     a.n_rows = n_rows_total > 0 ? n_rows_total : 0;
+    if (trk) {
+      a.trk = *trk;
+      a.trk.n0 = trk->n0 + (unsigned long long)start;
+    }
     hipEventRecord(evs[2 * li], st);
     hipError_t e = dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
       const long long threads = C * LPC;
@@ -507,6 +519,10 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
       return GM_EHIP;
     }
     hipEventRecord(evs[2 * li + 1], st);
+    if (hook && *hook) {
+      const int rc = (*hook)(start + nst);
+      if (rc) return rc;
+    }
   }
   ns.m += total;
   *step += (uint64_t)total + 1;  // +1: the init draw consumed a counter value

@@ -16,6 +16,9 @@ from ._sampler import Sampler
 
 
 class HMC(Sampler):
+    _progress_prefix = "HMC"
+    _progress_interval = 0.5  # seconds between progress reports
+
     def __init__(self, target, initial_positions, step_size: float, n_leapfrog: int,
                  dtype=None, chain_offset: int = 0):
         self._step_size = float(step_size)

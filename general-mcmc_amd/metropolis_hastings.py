@@ -11,6 +11,9 @@ from .distributions import IsotropicGaussian
 
 
 class MetropolisHastings(Sampler):
+    _progress_prefix = "Global"
+    _progress_interval = 1.0  # seconds between progress reports
+
     def __init__(self, target, proposal: IsotropicGaussian, initial_states, dtype=None,
                  chain_offset: int = 0):
         if not isinstance(proposal, IsotropicGaussian):
@@ -27,3 +30,9 @@ class MetropolisHastings(Sampler):
 
     def run(self, n_collect: int, n_discard: int) -> np.ndarray:
         return super().run(n_collect, n_discard).astype(np.float64, copy=False)
+
+    def run_progress(self, n_collect: int, n_discard: int, progress=None, interval=None):
+        """ChainRunner::run_progress (core.rs:251-403): f64 samples + RunStats,
+        with every chain's ChainTracker stepped on the device each transition."""
+        out, stats = super().run_progress(n_collect, n_discard, progress, interval)
+        return out.astype(np.float64, copy=False), stats

@@ -16,6 +16,9 @@ from ._sampler import Sampler
 
 
 class NUTS(Sampler):
+    _progress_prefix = "Global"
+    _progress_interval = 1.0  # seconds between progress reports
+
     def __init__(self, target, initial_positions, target_accept_p: float, dtype=None,
                  max_depth: int = 0, chain_offset: int = 0):
         self.target_accept_p = float(target_accept_p)

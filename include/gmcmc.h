@@ -223,6 +223,43 @@ int gm_split_rhat_ess_dist(gm_comm* comm, const void* dev_sample, gm_dtype dtype
                            int64_t stride_chain, int64_t stride_draw, int64_t stride_param,
                            float* rhat_out, float* ess_out);
 
+/* ---- run_progress with live statistics -------------------------------
+ * The reference's run_progress draws progress bars fed by chain trackers:
+ * HMC steps a MultiChainTracker with the current positions at most every
+ * 500 ms and at the last step (hmc.rs:245-306); ChainRunner (MH) and NUTS
+ * step a ChainTracker per chain after EVERY transition, burn-in included,
+ * and report collect_rhat over the chains every second (core.rs:132-176,
+ * 251-387; generic_nuts.rs:675-716). Here the trackers live on the device
+ * (MH / NUTS: fused into the sampling kernels) and `cb`, when not NULL, is
+ * called between launches at most every `interval_s` seconds and after the
+ * last transition. The returned samples and R-hat/ESS are those of
+ * gm_run_progress. */
+typedef struct gm_progress {
+  int64_t done;   /* transitions done (HMC: of the n_collect phase; MH/NUTS: of all) */
+  int64_t total;  /* HMC: n_collect; MH/NUTS: n_discard + n_collect */
+  float p_accept; /* HMC: MultiChainTracker::p_accept; MH/NUTS: mean over chains of
+                     the ChainTracker acceptance EMA */
+  float max_rhat; /* max over parameters of the tracker R-hat, NaN skipped
+                     (stats.rs:139-161, 298-317) */
+} gm_progress;
+typedef void (*gm_progress_fn)(void* user, const gm_progress* info);
+int gm_run_progress_cb(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out,
+                       float* rhat_out, float* ess_out, gm_progress_fn cb, void* user,
+                       double interval_s);
+/* ChainTracker::stats of every chain after an MH / NUTS run_progress
+ * (stats.rs:122-131): steps taken, p_accept [C], mean [C][dim], sm2 [C][dim]
+ * (any output may be NULL). */
+int gm_sampler_chain_stats(gm_sampler* s, uint64_t* n, float* p_accept, float* mean, float* sm2);
+
+/* MultiChainTracker (stats.rs:199-339) over [n_chains][n_params] device
+ * positions of either dtype. */
+typedef struct gm_mct gm_mct;
+int gm_mct_create(int64_t n_chains, int64_t n_params, gm_mct** out);
+int gm_mct_step(gm_mct* t, const void* dev_positions, gm_dtype dtype);
+/* p_accept, rhat [n_params] and max_rhat (any may be NULL) */
+int gm_mct_stats(gm_mct* t, float* p_accept, float* rhat, float* max_rhat);
+int gm_mct_destroy(gm_mct* t);
+
 /* ---- granular BatchVector ops (tier 2 of the boundary) ----------------
  * The reference's plug-in seam is the BatchVector trait implemented for
  * Tensor<B,2> [n_chains, dim] (euclidean.rs:145-195, 358-534) plus

@@ -507,6 +507,84 @@ void or_mct_rhat(const float* steps, int64_t nsteps, int64_t C, int64_t P, float
   free(mean_sq);
 }
 
+/* MultiChainTracker acceptance EMA (stats.rs:256-265): p starts at 0, and
+ * each step folds over the chains in order, accepted = row differs from the
+ * previous step's row (the first step compares against zeros). */
+float or_mct_p_accept(const float* steps, int64_t nsteps, int64_t C, int64_t P) {
+  const float alpha = 0.01f;
+  float p = 0.0f;
+  for (int64_t s = 0; s < nsteps; ++s)
+    for (int64_t c = 0; c < C; ++c) {
+      int diff = 0;
+      for (int64_t j = 0; j < P; ++j) {
+        const float prev = s ? steps[((s - 1) * C + c) * P + j] : 0.0f;
+        diff |= steps[(s * C + c) * P + j] != prev;
+      }
+      p = (1.0f - alpha) * p + alpha * (float)diff;
+    }
+  return p;
+}
+
+/* A batch of C ChainTrackers (stats.rs:24-131). or_ct_init = new(): n = 0,
+ * p_accept = -1, last_state = initial state, mean = mean_sq = 0.
+ * or_ct_step = step() with n the count after the increment. */
+void or_ct_init(int64_t C, int64_t P, const float* x0, float* p_accept, float* last, float* mean,
+                float* msq) {
+  for (int64_t c = 0; c < C; ++c) p_accept[c] = -1.0f;
+  for (int64_t i = 0; i < C * P; ++i) {
+    last[i] = x0[i];
+    mean[i] = 0.0f;
+    msq[i] = 0.0f;
+  }
+}
+void or_ct_step(int64_t C, int64_t P, uint64_t n_after, const float* x, float* p_accept, float* last,
+                float* mean, float* msq) {
+  const float alpha = 0.01f;
+  const float n = (float)n_after;
+  for (int64_t c = 0; c < C; ++c) {
+    const float* xc = x + c * P;
+    float* m = mean + c * P;
+    float* q = msq + c * P;
+    float* l = last + c * P;
+    for (int64_t j = 0; j < P; ++j) {
+      m[j] = (m[j] * (n - 1.0f) + xc[j]) / n;
+      q[j] = (n_after == 1) ? xc[j] * xc[j] : (q[j] * (n - 1.0f) + xc[j] * xc[j]) / n;
+    }
+    const float p_start = p_accept[c] >= 0.0f ? p_accept[c] : (float)(xc[0] != l[0]);
+    int diff = 0;
+    for (int64_t j = 0; j < P; ++j) diff |= xc[j] != l[j];
+    p_accept[c] = (1.0f - alpha) * p_start + alpha * (float)diff;
+    for (int64_t j = 0; j < P; ++j) l[j] = xc[j];
+  }
+}
+/* ChainTracker::stats (stats.rs:122-131) of every chain, then collect_rhat
+ * over them (stats.rs:139-193): between divides by (C*P - 1), the element
+ * count of the [C, P] difference array (diffs.len()). */
+void or_collect_rhat(int64_t C, int64_t P, uint64_t n_steps, const float* mean, const float* msq,
+                     float* rhat) {
+  const float n = (float)n_steps, nc = (float)C;
+  float nsum = 0.0f;
+  for (int64_t c = 0; c < C; ++c) nsum += n;
+  const float navg = nsum / nc;
+  for (int64_t p = 0; p < P; ++p) {
+    float within = 0.0f, gm = 0.0f, between = 0.0f;
+    for (int64_t c = 0; c < C; ++c) {
+      const float m = mean[c * P + p];
+      within += (msq[c * P + p] - m * m) * n / (n - 1.0f);
+    }
+    within /= nc;
+    for (int64_t c = 0; c < C; ++c) gm += mean[c * P + p];
+    gm /= nc;
+    for (int64_t c = 0; c < C; ++c) {
+      const float d = mean[c * P + p] - gm;
+      between += d * d;
+    }
+    between /= (float)(C * P - 1);
+    const float var = between + within * ((navg - 1.0f) / navg);
+    rhat[p] = sqrtf(var / within);
+  }
+}
+
 /* ===================== KAT entry points (double) ===================== */
 double or_find_reasonable_epsilon_d(const or_target* t, int lanes, int elems, const double* q,
                                     const double* p) {

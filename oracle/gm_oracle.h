@@ -103,6 +103,13 @@ void or_autocov_bf(const float* x, int64_t n, int64_t d, float* out);
 void or_autocov_fft(const float* x, int64_t n, int64_t d, float* out);
 /* MultiChainTracker: steps [nsteps][C][P] -> rhat [P] (stats.rs:199-339) */
 void or_mct_rhat(const float* steps, int64_t nsteps, int64_t C, int64_t P, float* rhat);
+float or_mct_p_accept(const float* steps, int64_t nsteps, int64_t C, int64_t P);
+void or_ct_init(int64_t C, int64_t P, const float* x0, float* p_accept, float* last, float* mean,
+                float* msq);
+void or_ct_step(int64_t C, int64_t P, uint64_t n_after, const float* x, float* p_accept, float* last,
+                float* mean, float* msq);
+void or_collect_rhat(int64_t C, int64_t P, uint64_t n_steps, const float* mean, const float* msq,
+                     float* rhat);
 
 #ifdef __cplusplus
 }

@@ -68,6 +68,11 @@ def load():
     lib.or_autocov_bf.argtypes = [_vp, _i64, _i64, _vp]
     lib.or_autocov_fft.argtypes = [_vp, _i64, _i64, _vp]
     lib.or_mct_rhat.argtypes = [_vp, _i64, _i64, _i64, _vp]
+    lib.or_mct_p_accept.restype = _flt
+    lib.or_mct_p_accept.argtypes = [_vp, _i64, _i64, _i64]
+    lib.or_ct_init.argtypes = [_i64, _i64, _vp, _vp, _vp, _vp, _vp]
+    lib.or_ct_step.argtypes = [_i64, _i64, _u64, _vp, _vp, _vp, _vp, _vp]
+    lib.or_collect_rhat.argtypes = [_i64, _i64, _u64, _vp, _vp, _vp]
     _lib = lib
     return Oracle(lib)
 
@@ -200,6 +205,31 @@ class Oracle:
         ns, c, p = s.shape
         r = np.empty(p, dtype=np.float32)
         self.lib.or_mct_rhat(_p(s), ns, c, p, _p(r))
+        return r
+
+    def mct_p_accept(self, steps):
+        """MultiChainTracker acceptance EMA after stepping [nsteps, C, P]."""
+        x = np.ascontiguousarray(steps, dtype=np.float32)
+        return self.lib.or_mct_p_accept(_p(x), *x.shape)
+
+    def chain_trackers(self, x0, states):
+        """A batch of ChainTrackers: new(x0 [C, P]) then step() with each of
+        states [n, C, P]; returns (p_accept [C], mean, msq [C, P])."""
+        x0 = np.ascontiguousarray(x0, dtype=np.float32)
+        C_, P = x0.shape
+        p = np.empty(C_, dtype=np.float32)
+        last, mean, msq = (np.empty((C_, P), dtype=np.float32) for _ in range(3))
+        self.lib.or_ct_init(C_, P, _p(x0), _p(p), _p(last), _p(mean), _p(msq))
+        for k, xs in enumerate(np.ascontiguousarray(states, dtype=np.float32)):
+            self.lib.or_ct_step(C_, P, k + 1, _p(np.ascontiguousarray(xs)), _p(p), _p(last), _p(mean),
+                                _p(msq))
+        return p, mean, msq
+
+    def collect_rhat(self, n, mean, msq):
+        mean = np.ascontiguousarray(mean, dtype=np.float32)
+        msq = np.ascontiguousarray(msq, dtype=np.float32)
+        r = np.empty(mean.shape[1], dtype=np.float32)
+        self.lib.or_collect_rhat(mean.shape[0], mean.shape[1], n, _p(mean), _p(msq), _p(r))
         return r
 
     def find_reasonable_epsilon(self, target: Target, q, p, lanes=64, elems=1):
