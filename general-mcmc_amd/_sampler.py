@@ -25,6 +25,14 @@ class DeviceSamples:
     def to_host(self) -> np.ndarray:
         return self.owner.copy_samples(self.n_collect)
 
+    def block(self, row0: int, n_rows: int, chain0: int, n_chains: int) -> np.ndarray:
+        """Rows [row0, row0+n_rows) x chains [chain0, chain0+n_chains) on the
+        host, [n_rows, n_chains, dim] (one strided device-to-host copy)."""
+        out = np.empty((n_rows, n_chains, self.dim), dtype=self.dtype)
+        _lib.check(self.owner._lib.gm_copy_sample_block(self.owner._h, row0, n_rows, chain0, n_chains,
+                                                        _lib.ptr(out)))
+        return out
+
     def split_rhat_ess(self):
         return split_rhat_mean_ess_device(self.ptr, self.dtype, self.n_chains, self.n_collect,
                                           self.dim, (self.dim, self.n_chains * self.dim, 1))

@@ -631,6 +631,21 @@ int gm_copy_samples(gm_sampler* s, void* out) {
   return GM_OK;
 }
 
+int gm_copy_sample_block(gm_sampler* s, int64_t row0, int64_t n_rows, int64_t chain0, int64_t n_chains,
+                         void* out) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(row0 >= 0 && n_rows >= 0 && row0 + n_rows <= s->last_rows, "rows out of range of the last run");
+  GM_REQ(chain0 >= 0 && n_chains >= 0 && chain0 + n_chains <= s->C, "chains out of range");
+  if (n_rows == 0 || n_chains == 0) return GM_OK;
+  GM_REQ(out != nullptr, "out is NULL");
+  GM_HIP(hipSetDevice(s->device));
+  const size_t row_bytes = (size_t)s->C * s->D * s->esz, w = (size_t)n_chains * s->D * s->esz;
+  const char* src = (const char*)s->d_samples + (size_t)row0 * row_bytes + (size_t)chain0 * s->D * s->esz;
+  GM_HIP(hipMemcpy2DAsync(out, w, src, row_bytes, w, (size_t)n_rows, hipMemcpyDeviceToHost, s->stream));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  return GM_OK;
+}
+
 int gm_run(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out) {
   int rc = run_impl(s, n_collect, n_discard, 0);
   if (rc) return rc;

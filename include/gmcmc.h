@@ -162,6 +162,13 @@ int gm_run_progress(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* o
 int gm_copy_samples(gm_sampler* s, void* out);
 
 /* positions() (hmc.rs:326-328): host [n_chains][dim]. */
+/* A block of the last run's device samples, rows [row0, row0+n_rows) x
+ * chains [chain0, chain0+n_chains), copied to the host as
+ * [n_rows][n_chains][dim] (one strided copy): the streaming egress used by
+ * the CSV / Arrow / Parquet writers (io/*.rs) so that a sample larger than
+ * host memory never has to exist there whole. */
+int gm_copy_sample_block(gm_sampler* s, int64_t row0, int64_t n_rows, int64_t chain0, int64_t n_chains,
+                         void* out);
 int gm_get_positions(gm_sampler* s, void* out);
 int gm_set_positions(gm_sampler* s, const void* in);
 

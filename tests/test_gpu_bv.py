@@ -118,3 +118,25 @@ def test_bv_rejects_bad_arguments(gm, bv):
         bv.add_scaled_assign(a, b, 1.0)
     lib = gm._lib.load()
     assert lib.gm_bv_kinetic_energy(7, 4, 3, None, None) == gm._lib.GM_EINVAL  # bad dtype
+
+
+def test_writers_stream_device_samples(gm, tmp_path, monkeypatch):
+    """io writers on DeviceSamples (streamed by blocks) == on the host copy."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    import general_mcmc_amd.io as gio
+    s = gm.HMC(gm.RosenbrockND(), gm.init_with_seed(37, 5, 3, np.float32), 0.02, 4).set_seed(2)
+    ds = s.run_positions(11, 2)
+    host = ds.to_host()  # [C, N, D]
+    np.testing.assert_array_equal(ds.block(3, 4, 5, 9), host[5:14, 3:7].transpose(1, 0, 2))
+    monkeypatch.setattr(gio, "_CHAIN_BLOCK_BYTES", 700)  # several blocks
+    for name, fn in (("a.arrow", gio.save_arrow), ("p.parquet", gio.save_parquet), ("c.csv", gio.save_csv)):
+        fn(ds, str(tmp_path / ("d" + name)))
+        fn(host, str(tmp_path / ("h" + name)))
+    assert (tmp_path / "dc.csv").read_text() == (tmp_path / "hc.csv").read_text()
+    assert pa.ipc.open_file(str(tmp_path / "da.arrow")).read_all().equals(
+        pa.ipc.open_file(str(tmp_path / "ha.arrow")).read_all())
+    assert pq.read_table(str(tmp_path / "dp.parquet")).equals(pq.read_table(str(tmp_path / "hp.parquet")))
+    gio.save_parquet_tensor(ds, str(tmp_path / "dt.parquet"))
+    gio.save_parquet_tensor(host.transpose(1, 0, 2), str(tmp_path / "ht.parquet"))
+    assert pq.read_table(str(tmp_path / "dt.parquet")).equals(pq.read_table(str(tmp_path / "ht.parquet")))
