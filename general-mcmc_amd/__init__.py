@@ -12,7 +12,7 @@ from .distributions import (DenseGaussian, DiffableGaussian2D, Gaussian2D, Isotr
                             Rosenbrock2D, RosenbrockND)
 from .hmc import HMC
 from .metropolis_hastings import MetropolisHastings
-from .nuts import NUTS, NUTSChain
+from .nuts import NUTS, MassMatrix, NUTSChain, NUTSMassMatrixConfig
 from .stats import (BasicStats, ChainStats, MultiChainTracker, Progress, RunStats, basic_stats,
                     split_rhat_mean_ess)
 
@@ -20,5 +20,5 @@ __all__ = [
     "HMC", "NUTS", "NUTSChain", "MetropolisHastings", "RosenbrockND", "Rosenbrock2D",
     "IsotropicGaussian", "DiffableGaussian2D", "DenseGaussian", "Gaussian2D", "init", "init_det",
     "init_with_seed", "split_rhat_mean_ess", "basic_stats", "BasicStats", "RunStats", "GMError",
-    "batch_vector", "MultiChainTracker", "ChainStats", "Progress",
+    "batch_vector", "MultiChainTracker", "ChainStats", "Progress", "NUTSMassMatrixConfig", "MassMatrix",
 ]

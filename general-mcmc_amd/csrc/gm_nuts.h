@@ -25,6 +25,22 @@ struct NutsState {
   long long* n_leapfrog = nullptr;  // [C] cumulative leapfrog count
   long long m = 0;            // transitions since the last init_chain_state (:735)
   long long n_discard = 0;    // warm-up length of the current run (:734)
+  // mass-matrix warm-up (GenericNUTS::new_with_mass_matrix, generic_nuts.rs:33-359)
+  int mass_mode = 0;          // 0 off (identity), 1 diagonal, 2 dense
+  long long m_sb = 0, m_eb = 0;
+  double m_reg = 0, m_jit = 0;
+  long long sched_next = 0, sched_len = 0;  // MassMatrixWarmup window schedule (persists)
+  int* mkind = nullptr;       // [C] 0 identity, 1 diagonal, 2 dense
+  void* dinv = nullptr;       // [C][D]
+  void* dsq = nullptr;        // [C][D]
+  void* minv = nullptr;       // [C][D][D]
+  void* mchol = nullptr;      // [C][D][D]
+  int* rn = nullptr;          // [C] RunningCov
+  void* rmean = nullptr;      // [C][D]
+  void* rm2d = nullptr;       // [C][D]
+  void* rm2 = nullptr;        // [C][D][D]
+  int* updated = nullptr;     // [C]
+  void* mscratch = nullptr;   // [C][4][D][D] dense update workspace
 };
 
 int nuts_init_state(NutsState* ns, gm_dtype dt, long long C, int D, int max_depth);
@@ -39,6 +55,10 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
              long long n_discard, int progress, long long steps_per_launch, hipStream_t st,
              std::vector<hipEvent_t>& evs, double* ms, long long* launches,
              const TrackLaunch* trk = nullptr, const StepHook* hook = nullptr);
+int nuts_set_mass(NutsState* ns, gm_dtype dt, long long C, int D, int mode, long long start_buffer,
+                  long long end_buffer, long long initial_window, double regularize, double jitter);
+int nuts_get_mass(NutsState& ns, gm_dtype dt, long long C, int D, int32_t* kind, void* dinv, void* dsqrt,
+                  void* minv, void* mchol);
 int nuts_get_step_size(NutsState& ns, gm_dtype dt, long long C, double* eps, double* eps_bar);
 int nuts_get_leapfrogs(NutsState& ns, long long C, long long* out);
 

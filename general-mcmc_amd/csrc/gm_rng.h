@@ -53,7 +53,8 @@ enum : uint32_t {
   TAG_NUTS_DIR = 8,  // NUTS direction uniform (generic_nuts.rs:783)
   TAG_NUTS_TOP = 9,  // NUTS top-level accept uniform (generic_nuts.rs:865)
   TAG_NUTS_MRG = 10, // NUTS subtree-merge f64 uniform (generic_nuts.rs:1305)
-  TAG_NUTS_INIT = 11 // NUTS init momentum for find_reasonable_epsilon (:739)
+  TAG_NUTS_INIT = 11, // NUTS init momentum for find_reasonable_epsilon (:739)
+  TAG_NUTS_PROBE = 12 // NUTS probe momentum after a mass-matrix update (:905-909)
 };
 
 struct u32x4 { uint32_t x, y, z, w; };

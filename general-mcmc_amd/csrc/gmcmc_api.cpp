@@ -844,6 +844,31 @@ int gm_nuts_get_step_size(gm_sampler* s, double* eps, double* eps_bar) {
   return nuts_get_step_size(s->nuts, s->dt, s->C, eps, eps_bar);
 }
 
+int gm_nuts_set_mass_adaptation(gm_sampler* s, int32_t mode, int64_t start_buffer, int64_t end_buffer,
+                                int64_t initial_window, double regularize, double jitter,
+                                int64_t dense_max_dim) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");
+  GM_REQ(mode >= 0 && mode <= 2, "mode must be 0 (none), 1 (diagonal) or 2 (dense)");
+  GM_REQ(start_buffer >= 0 && end_buffer >= 0 && initial_window >= 0, "window sizes must be >= 0");
+  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  // dense only up to dense_max_dim, else diagonal (generic_nuts.rs:613-620)
+  if (mode == 2 && s->D > dense_max_dim) mode = 1;
+  return nuts_set_mass(&s->nuts, s->dt, s->C, s->D, mode, start_buffer, end_buffer, initial_window,
+                       regularize, jitter);
+}
+
+int gm_nuts_get_mass(gm_sampler* s, int32_t* mode, int32_t* kind, void* dinv, void* dsqrt, void* minv,
+                     void* mchol) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");
+  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  if (mode) *mode = s->nuts.mass_mode;
+  return nuts_get_mass(s->nuts, s->dt, s->C, s->D, kind, dinv, dsqrt, minv, mchol);
+}
+
 struct gm_mct {
   long long C = 0;
   int P = 0;

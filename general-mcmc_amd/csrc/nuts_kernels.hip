@@ -13,9 +13,10 @@
 // The reference's recursive build_tree is evaluated here iteratively: leaves
 // are integrated in trajectory order and a completed subtree is merged with
 // the stored left sibling of its level, which performs the merges (and their
-// random draws) in exactly the recursion's post-order. A truncated left
-// subtree (s' = false) ends the build without a merge, a truncated right
-// subtree still merges -- again as the recursion does.
+// random draws) in exactly the recursion's post-order. A truncated subtree
+// (s' = false) stops the leaf integration, and is still merged into every
+// enclosing subtree of which it is (part of) the right half, as the
+// recursion returns it upward.
 //
 // One lane group (LPC lanes x E coordinates) owns one chain; chains follow
 // their own control flow. The per-level stack of stored left subtrees lives in
@@ -56,7 +57,94 @@ struct NutsLaunch {
   long long row_shift = 0;   // state after t transitions goes to row t - row_shift
   long long n_rows = 0;
   TrackLaunch trk;           // run_progress chain trackers (off when trk.mean is null)
+  // mass-matrix warm-up (generic_nuts.rs:33-359); mass_mode 0 = identity, off
+  int mass_mode = 0;         // 1 diagonal, 2 dense
+  int* mkind = nullptr;      // [C] current metric of each chain: 0 identity, 1 diag, 2 dense
+  void* dinv = nullptr;      // [C][D]
+  void* dsq = nullptr;       // [C][D]
+  void* minv = nullptr;      // [C][D][D]
+  void* mchol = nullptr;     // [C][D][D]
+  int* rn = nullptr;         // [C] RunningCov::n
+  void* rmean = nullptr;     // [C][D]
+  void* rm2d = nullptr;      // [C][D]
+  void* rm2 = nullptr;       // [C][D][D] (upper triangle used)
+  int* updated = nullptr;    // [C] metric replaced at the previous launch's last step
+  long long sb = 0, eb = 0;  // start_buffer, end_buffer (should_collect, :153-162)
+  int do_refind = 0;         // re-find eps for updated chains first (:905-918)
+  uint64_t refind_step = 0;  // transition index of the update (probe draws)
 };
+
+// coordinate j of a chain's vector: lane j/E of the group, slot j%E
+template <int LPC, int E, class T>
+__device__ __forceinline__ T coord(const T (&x)[E], int j) {
+  const int src = j / E, slot = j % E;
+  T mine = x[0];
+#pragma unroll
+  for (int e = 1; e < E; ++e) mine = (slot == e) ? x[e] : mine;
+  if constexpr (LPC == 1) return mine;
+  else return __shfl(mine, src, LPC);
+}
+
+// MassMatrix (generic_nuts.rs:175-304) of one chain, this lane's view
+template <class T, int E> struct MassDev {
+  int kind = 0;             // 0 identity, 1 diagonal, 2 dense
+  T inv[E], sq[E];          // diagonal
+  const T* minv = nullptr;  // dense [D][D]
+  const T* chol = nullptr;
+  int D = 0;
+};
+
+// inv_mul (:255-273): v = M^-1 p
+template <int LPC, int E, class T>
+__device__ __forceinline__ void inv_mul(const MassDev<T, E>& M, const T (&p)[E], T (&v)[E], int lane) {
+  if (M.kind == 1) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = M.inv[e] * p[e];
+  } else if (M.kind == 2) {
+    T acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = (T)0;
+    for (int j = 0; j < M.D; ++j) {
+      const T pj = coord<LPC, E>(p, j);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        if (i < M.D) acc[e] = acc[e] + M.minv[(long long)i * M.D + j] * pj;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = acc[e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = p[e];
+  }
+}
+
+// sample_momentum (:275-303) applied to standard normals z
+template <int LPC, int E, class T>
+__device__ __forceinline__ void momentum_from(const MassDev<T, E>& M, const T (&z)[E], T (&p)[E], int lane) {
+  if (M.kind == 1) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) p[e] = z[e] * M.sq[e];
+  } else if (M.kind == 2) {
+    T acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = (T)0;
+    for (int j = 0; j < M.D; ++j) {
+      const T zj = coord<LPC, E>(z, j);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        if (i < M.D && j <= i) acc[e] = acc[e] + M.chol[(long long)i * M.D + j] * zj;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) p[e] = acc[e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) p[e] = z[e];
+  }
+}
 
 template <int LPC, int E, class T>
 __device__ __forceinline__ T dot_group(const T (&a)[E], const T (&b)[E]) {
@@ -96,6 +184,59 @@ __device__ __forceinline__ bool no_uturn(const T (&qm)[E], const T (&qp)[E], con
   for (int e = 0; e < E; ++e) d[e] = qp[e] - qm[e];
   const T dm = dot_group<LPC, E>(d, pm);
   const T dp = dot_group<LPC, E>(d, pp);
+  return dm >= (T)0 && dp >= (T)0;
+}
+
+// MassMatrix::kinetic (:226-253), canonical-order sum of the per-coordinate
+// terms p*p*inv (diagonal) or p_i (M^-1 p)_i (dense)
+template <int LPC, int E, class T>
+__device__ __forceinline__ T kinetic_m(const MassDev<T, E>& M, const T (&p)[E], int lane) {
+  if (M.kind == 0) return kinetic<LPC, E>(p);
+  T t[E];
+  if (M.kind == 1) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) t[e] = p[e] * p[e] * M.inv[e];
+  } else {
+    inv_mul<LPC, E>(M, p, t, lane);
+#pragma unroll
+    for (int e = 0; e < E; ++e) t[e] = p[e] * t[e];
+  }
+  T part = t[0];
+#pragma unroll
+  for (int e = 1; e < E; ++e) part = part + t[e];
+  return (T)0.5 * group_sum<LPC>(part);
+}
+
+// leapfrog_with_mass (:1396-1418): drift by M^-1 p
+template <int LPC, int E, class T, class TG>
+__device__ __forceinline__ T leapfrog_m(const TG& tg, const MassDev<T, E>& M, T (&q)[E], T (&p)[E],
+                                        T (&g)[E], T epsv, int lane) {
+  if (M.kind == 0) return leapfrog<LPC, E>(tg, q, p, g, epsv, lane);
+  const T h = epsv * (T)0.5;
+#pragma unroll
+  for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
+  T v[E];
+  inv_mul<LPC, E>(M, p, v, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) q[e] = q[e] + v[e] * epsv;
+  const T lp = tg.template eval<LPC, E, true>(q, g, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
+  return lp;
+}
+
+// stop_criterion_with_mass (:1354-1378), the top-level U-turn
+template <int LPC, int E, class T>
+__device__ __forceinline__ bool no_uturn_m(const MassDev<T, E>& M, const T (&qm)[E], const T (&qp)[E],
+                                           const T (&pm)[E], const T (&pp)[E], int lane) {
+  if (M.kind == 0) return no_uturn<LPC, E>(qm, qp, pm, pp);
+  T d[E], vm[E], vp[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) d[e] = qp[e] - qm[e];
+  inv_mul<LPC, E>(M, pm, vm, lane);
+  inv_mul<LPC, E>(M, pp, vp, lane);
+  const T dm = dot_group<LPC, E>(d, vm);
+  const T dp = dot_group<LPC, E>(d, vp);
   return dm >= (T)0 && dp >= (T)0;
 }
 
@@ -185,16 +326,52 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   const T gamma = (T)0.05, kappa = (T)0.75, delta = (T)a.target_accept;
   const long long t0c = 10;
 
-  if (a.do_init) {  // init_chain_state (generic_nuts.rs:731-753)
-    T p0[E];
+  // the chain's metric and warm-up statistics (generic_nuts.rs:33-359)
+  MassDev<T, E> M;
+  M.D = D;
+  int rn = 0;
+  T rmean[E], rm2d[E];
+  if (a.mass_mode) {
+    M.kind = a.mkind[c];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
-      p0[e] = (i < D) ? normal<T>(a.seed, cid, a.init_step, TAG_NUTS_INIT, (uint32_t)i) : (T)0;
+      M.inv[e] = (i < D) ? ((const T*)a.dinv)[c * D + i] : (T)0;
+      M.sq[e] = (i < D) ? ((const T*)a.dsq)[c * D + i] : (T)0;
+      rmean[e] = (i < D) ? ((const T*)a.rmean)[c * D + i] : (T)0;
+      rm2d[e] = (i < D) ? ((const T*)a.rm2d)[c * D + i] : (T)0;
     }
+    if (a.mass_mode == 2) {
+      M.minv = (const T*)a.minv + (long long)c * D * D;
+      M.chol = (const T*)a.mchol + (long long)c * D * D;
+    }
+    rn = a.rn[c];
+  }
+
+  if (a.do_init) {  // init_chain_state (generic_nuts.rs:731-753)
+    T z[E], p0[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      z[e] = (i < D) ? normal<T>(a.seed, cid, a.init_step, TAG_NUTS_INIT, (uint32_t)i) : (T)0;
+    }
+    momentum_from<LPC, E>(M, z, p0, lane);
     const T ae = eps + (T)1;
     if ((ae < (T)0 ? -ae : ae) <= MachEps<T>::v) eps = find_reasonable_epsilon<LPC, E>(tg, q, p0, lane, D);
     mu = glog((T)10 * eps);
+  }
+  if (a.do_refind && a.updated[c]) {  // after a metric update (generic_nuts.rs:905-918)
+    T z[E], probe[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      z[e] = (i < D) ? normal<T>(a.seed, cid, a.refind_step, TAG_NUTS_PROBE, (uint32_t)i) : (T)0;
+    }
+    momentum_from<LPC, E>(M, z, probe, lane);
+    eps = find_reasonable_epsilon<LPC, E>(tg, q, probe, lane, D);  // identity-mass leapfrog (:1009-1023)
+    mu = glog((T)10 * eps);
+    eps_bar = eps;
+    h_bar = (T)0;
   }
   auto record = [&](long long t) {
     const long long row = t - a.row_shift;
@@ -219,13 +396,17 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     const long long m = a.m0 + s + 1;
     // --- momentum, slice (generic_nuts.rs:758-768)
     T p0[E], g0[E];
+    {
+      T z[E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int i = lane * E + e;
-      p0[e] = (i < D) ? ncache[e].get(a.seed, cid, st, TAG_NUTS_MOM, (uint32_t)i) : (T)0;
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        z[e] = (i < D) ? ncache[e].get(a.seed, cid, st, TAG_NUTS_MOM, (uint32_t)i) : (T)0;
+      }
+      momentum_from<LPC, E>(M, z, p0, lane);
     }
     const T logp0 = tg.template eval<LPC, E, true>(q, g0, lane);
-    const T joint0 = logp0 - kinetic<LPC, E>(p0);
+    const T joint0 = logp0 - kinetic_m<LPC, E>(M, p0, lane);
     const T logu = joint0 - exp1<T>(a.seed, cid, st, TAG_NUTS_EXP, 0u);
     // trajectory ends
     T qm[E], pm[E], gm_[E], qp[E], pp[E], gp[E];
@@ -261,9 +442,9 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       long long tna = 0;
       const long long nleaves = 1LL << j;
       for (long long l = 0; l < nleaves; ++l) {
-        const T lp = leapfrog<LPC, E>(tg, qe, pe, ge, epsv, lane);
+        const T lp = leapfrog_m<LPC, E>(tg, M, qe, pe, ge, epsv, lane);
         ++nlf;
-        const T joint = lp - kinetic<LPC, E>(pe);
+        const T joint = lp - kinetic_m<LPC, E>(M, pe, lane);
         tn = (logu < joint) ? 1 : 0;
         ts = (logu - (T)1000) < joint;
         ta = rust_min1(gexp(joint - joint0));
@@ -275,7 +456,10 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
         while (true) {
           if (k == j) { done = true; break; }
           if (((l >> k) & 1) == 0) {  // left child at level k
-            if (!ts) { done = true; break; }
+            // A truncated left subtree: its parent builds no right half and
+            // returns it unchanged; going up, it is merged wherever that
+            // parent is itself a right child (the recursion's post-order).
+            if (!ts) { ++k; continue; }
             T* sv = svec + ((long long)(k * 3) * C + c) * D;
 #pragma unroll
             for (int e = 0; e < E; ++e) {
@@ -338,7 +522,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
         ++acc;
       }
       n += tn;
-      s_ok = ts && no_uturn<LPC, E>(qm, qp, pm, pp);
+      s_ok = ts && no_uturn_m<LPC, E>(M, qm, qp, pm, pp, lane);
       ++j;
     }
     // dual averaging (generic_nuts.rs:882-924)
@@ -349,6 +533,31 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       eps = gexp(mu - gsqrt(mf) / gamma * h_bar);
       eta = gexp(-kappa * glog(mf));  // m^(-kappa)
       eps_bar = gexp(((T)1 - eta) * glog(eps_bar) + eta * glog(eps));
+      // RunningCov::update inside the collection window (:897-903, 108-129)
+      const long long lim = a.n_discard > a.eb ? a.n_discard - a.eb : 0;
+      if (a.mass_mode && m > a.sb && m < lim) {
+        rn += 1;
+        const T ns = (T)rn;
+        T d1[E], d2[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          d1[e] = q[e] - rmean[e];
+          rmean[e] = rmean[e] + d1[e] / ns;
+          d2[e] = q[e] - rmean[e];
+          rm2d[e] = rm2d[e] + d1[e] * d2[e];
+        }
+        if (a.mass_mode == 2) {
+          T* m2 = (T*)a.rm2 + (long long)c * D * D;
+          for (int jj = 0; jj < D; ++jj) {
+            const T dj = coord<LPC, E>(d2, jj);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+              const int i = lane * E + e;
+              if (i < D && jj >= i) m2[(long long)i * D + jj] = m2[(long long)i * D + jj] + d1[e] * dj;
+            }
+          }
+        }
+      }
     } else {
       eps = eps_bar;
     }
@@ -356,6 +565,17 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     record(a.t0 + s + 1);
   }
   if (track) tr.store(a.trk, c, lane, D);
+  if (a.mass_mode) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      if (i < D) {
+        ((T*)a.rmean)[c * D + i] = rmean[e];
+        ((T*)a.rm2d)[c * D + i] = rm2d[e];
+      }
+    }
+    if (lane == 0) a.rn[c] = rn;
+  }
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int i = lane * E + e;
@@ -368,6 +588,131 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     ((T*)a.mu)[c] = mu;
     a.accepts[c] += acc;
     a.n_leapfrog[c] += nlf;
+  }
+}
+
+// ---- metric update at a window end (generic_nuts.rs:948-997, 175-359) ----
+// One thread per chain, the reference's sequential arithmetic.
+template <class T> __device__ __forceinline__ T rust_max(T a, T b) {  // Float::max
+  return (a != a) ? b : (b != b) ? a : (a > b ? a : b);
+}
+template <class T> __device__ bool cholesky_spd(const T* a, int dim, T* l) {
+  for (int i = 0; i < dim * dim; ++i) l[i] = (T)0;
+  for (int i = 0; i < dim; ++i)
+    for (int j = 0; j <= i; ++j) {
+      T sum = a[i * dim + j];
+      for (int k = 0; k < j; ++k) sum = sum - l[i * dim + k] * l[j * dim + k];
+      if (i == j) {
+        if (sum <= (T)0 || !(sum - sum == (T)0)) return false;
+        l[i * dim + j] = gsqrt(sum);
+      } else {
+        const T d = l[j * dim + j];
+        if (d <= (T)0 || !(d - d == (T)0)) return false;
+        l[i * dim + j] = sum / d;
+      }
+    }
+  return true;
+}
+template <class T> __device__ bool invert_spd_from_cholesky(const T* l, int dim, T* inv, T* inv_l) {
+  for (int i = 0; i < dim * dim; ++i) inv_l[i] = (T)0;
+  for (int i = 0; i < dim; ++i) {
+    const T d = l[i * dim + i];
+    if (d <= (T)0 || !(d - d == (T)0)) return false;
+    inv_l[i * dim + i] = (T)1 / d;
+    for (int j = i + 1; j < dim; ++j) {
+      T sum = (T)0;
+      for (int k = i; k < j; ++k) sum = sum + l[j * dim + k] * inv_l[k * dim + i];
+      inv_l[j * dim + i] = -sum / l[j * dim + j];
+    }
+  }
+  for (int i = 0; i < dim; ++i)
+    for (int j = 0; j <= i; ++j) {
+      T sum = (T)0;
+      for (int k = (i > j ? i : j); k < dim; ++k) sum = sum + inv_l[k * dim + i] * inv_l[k * dim + j];
+      inv[i * dim + j] = sum;
+      inv[j * dim + i] = sum;
+    }
+  return true;
+}
+template <class T>
+__device__ void diag_from_var(const T* var, int D, T jitter, T* inv, T* sq) {  // :205-216
+  for (int i = 0; i < D; ++i) {
+    const T v = rust_max(var[i], jitter);
+    inv[i] = (T)1 / v;
+    sq[i] = gsqrt(v);
+  }
+}
+
+template <class T>
+__global__ void nuts_mass_update_kernel(long long C, int D, int mode, double regularize, double jitter_cfg,
+                                        int* __restrict__ mkind, T* dinv, T* dsq, T* minv, T* mchol,
+                                        int* __restrict__ rn, T* rmean, T* rm2d, T* rm2,
+                                        int* __restrict__ updated, T* scratch /* [C][4][D][D] */) {
+  const long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  updated[c] = 0;
+  const int n = rn[c];
+  if (n < 5) return;  // maybe_update_mass_matrix: None
+  const T nd = (T)(n - 1);
+  const T reg = (T)regularize;
+  const T omr = (T)1 - reg;
+  const T jitter = (T)(jitter_cfg > 1e-10 ? jitter_cfg : 1e-10);
+  T* di = dinv + c * D;
+  T* ds = dsq + c * D;
+  bool ok = false;
+  if (mode == 1) {
+    T* var = rmean + c * D;  // the running stats are reset below; reuse mean as scratch
+    const T* m2d = rm2d + c * D;
+    for (int i = 0; i < D; ++i) var[i] = rust_max(omr * (m2d[i] / nd) + reg, jitter);
+    diag_from_var(var, D, jitter, di, ds);
+    mkind[c] = 1;
+    ok = true;
+  } else {
+    const long long DD = (long long)D * D;
+    T* cov = scratch + c * 4 * DD;
+    T* tr = cov + DD;
+    T* chol = tr + DD;
+    T* il = chol + DD;
+    const T* m2 = rm2 + c * DD;
+    for (int i = 0; i < D; ++i)
+      for (int j = i; j < D; ++j) {
+        const T raw = m2[i * D + j] / nd;
+        const T v = (i == j) ? rust_max(omr * raw + reg, jitter) : omr * raw;
+        cov[i * D + j] = v;
+        cov[j * D + i] = v;
+      }
+    // dense_from_cov (:218-236): up to 8 tries with a growing diagonal jitter
+    T jj = rust_max(jitter, (T)1e-10);
+    T* inv = minv + c * DD;
+    for (int t = 0; t < 8 && !ok; ++t) {
+      for (long long k = 0; k < DD; ++k) tr[k] = cov[k];
+      for (int d = 0; d < D; ++d) tr[d * D + d] = tr[d * D + d] + jj;
+      if (cholesky_spd(tr, D, chol) && invert_spd_from_cholesky(chol, D, tr, il)) ok = true;
+      else jj = jj * (T)10;
+    }
+    if (ok) {
+      for (long long k = 0; k < DD; ++k) {
+        inv[k] = tr[k];
+        mchol[c * DD + k] = chol[k];
+      }
+      mkind[c] = 2;
+    } else if (mkind[c] == 0) {  // identity -> diagonal_from_var(ones)
+      T* var = cov;
+      for (int i = 0; i < D; ++i) var[i] = (T)1;
+      diag_from_var(var, D, jitter, di, ds);
+      mkind[c] = 1;
+      ok = true;
+    }
+  }
+  if (ok) {  // RunningCov::reset after a successful update (:920)
+    updated[c] = 1;
+    rn[c] = 0;
+    for (int i = 0; i < D; ++i) {
+      rmean[c * D + i] = (T)0;
+      rm2d[c * D + i] = (T)0;
+    }
+    if (mode == 2)
+      for (long long k = 0; k < (long long)D * D; ++k) rm2[c * (long long)D * D + k] = (T)0;
   }
 }
 
@@ -417,7 +762,90 @@ static void ffree(void* p) {
   if (p) hipFree(p);
 }
 
+static void mass_free(NutsState* ns) {
+  ffree(ns->mkind);
+  ffree(ns->dinv);
+  ffree(ns->dsq);
+  ffree(ns->minv);
+  ffree(ns->mchol);
+  ffree(ns->rn);
+  ffree(ns->rmean);
+  ffree(ns->rm2d);
+  ffree(ns->rm2);
+  ffree(ns->updated);
+  ffree(ns->mscratch);
+  ns->mkind = ns->rn = ns->updated = nullptr;
+  ns->dinv = ns->dsq = ns->minv = ns->mchol = ns->rmean = ns->rm2d = ns->rm2 = ns->mscratch = nullptr;
+  ns->mass_mode = 0;
+}
+
+int nuts_set_mass(NutsState* ns, gm_dtype dt, long long C, int D, int mode, long long start_buffer,
+                  long long end_buffer, long long initial_window, double regularize, double jitter) {
+  mass_free(ns);
+  if (mode == 0) return GM_OK;
+  const size_t esz = dt == GM_F32 ? 4 : 8;
+  const size_t cd = (size_t)C * D * esz, cdd = (size_t)C * D * D * esz;
+  hipError_t e = hipMalloc((void**)&ns->mkind, C * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&ns->dinv, cd);
+  if (e == hipSuccess) e = hipMalloc(&ns->dsq, cd);
+  if (e == hipSuccess) e = hipMalloc((void**)&ns->rn, C * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc(&ns->rmean, cd);
+  if (e == hipSuccess) e = hipMalloc(&ns->rm2d, cd);
+  if (e == hipSuccess) e = hipMalloc((void**)&ns->updated, C * sizeof(int));
+  if (mode == 2) {
+    if (e == hipSuccess) e = hipMalloc(&ns->minv, cdd);
+    if (e == hipSuccess) e = hipMalloc(&ns->mchol, cdd);
+    if (e == hipSuccess) e = hipMalloc(&ns->rm2, cdd);
+    if (e == hipSuccess) e = hipMalloc(&ns->mscratch, 4 * cdd);
+  }
+  if (e != hipSuccess) {
+    mass_free(ns);
+    set_error(std::string("mass-matrix state allocation failed: ") + hipGetErrorString(e));
+    return GM_ENOMEM;
+  }
+  hipMemset(ns->mkind, 0, C * sizeof(int));  // MassMatrix::identity
+  hipMemset(ns->dinv, 0, cd);
+  hipMemset(ns->dsq, 0, cd);
+  if (mode == 2) {
+    hipMemset(ns->minv, 0, cdd);
+    hipMemset(ns->mchol, 0, cdd);
+  }
+  ns->mass_mode = mode;
+  ns->m_sb = start_buffer;
+  ns->m_eb = end_buffer;
+  ns->m_reg = regularize;
+  ns->m_jit = jitter;
+  // MassMatrixWarmup::new (generic_nuts.rs:141-151)
+  ns->sched_len = initial_window > 10 ? initial_window : 10;
+  ns->sched_next = (start_buffer > 1 ? start_buffer : 1) + ns->sched_len;
+  return hipDeviceSynchronize() == hipSuccess ? GM_OK : GM_EHIP;
+}
+
+int nuts_get_mass(NutsState& ns, gm_dtype dt, long long C, int D, int32_t* kind, void* dinv, void* dsqrt,
+                  void* minv, void* mchol) {
+  const size_t esz = dt == GM_F32 ? 4 : 8;
+  if (!ns.mass_mode) {
+    if (kind)
+      for (long long c = 0; c < C; ++c) kind[c] = 0;
+    return GM_OK;
+  }
+  hipError_t e = hipSuccess;
+  if (kind) e = hipMemcpy(kind, ns.mkind, C * sizeof(int), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && dinv) e = hipMemcpy(dinv, ns.dinv, (size_t)C * D * esz, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && dsqrt) e = hipMemcpy(dsqrt, ns.dsq, (size_t)C * D * esz, hipMemcpyDeviceToHost);
+  if (ns.mass_mode == 2) {
+    if (e == hipSuccess && minv) e = hipMemcpy(minv, ns.minv, (size_t)C * D * D * esz, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && mchol) e = hipMemcpy(mchol, ns.mchol, (size_t)C * D * D * esz, hipMemcpyDeviceToHost);
+  }
+  if (e != hipSuccess) {
+    set_error(std::string("mass-matrix copy failed: ") + hipGetErrorString(e));
+    return GM_EHIP;
+  }
+  return GM_OK;
+}
+
 void nuts_free_state(NutsState* ns) {
+  mass_free(ns);
   ffree(ns->eps);
   ffree(ns->eps_bar);
   ffree(ns->h_bar);
@@ -460,9 +888,50 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
   const uint64_t init_step = *step;
   const long long n_rows_total = progress ? total - n_discard : total - n_discard + 1;
   const long long row_shift = progress ? n_discard + 1 : n_discard;
+  // Launch segments: at most steps_per_launch transitions each, and a
+  // segment also ends at every warm-up window end, after which the metric
+  // update kernel runs and the next segment starts with the probe + epsilon
+  // re-find (generic_nuts.rs:897-921). The window schedule depends on m and
+  // n_discard only, so it is the same for every chain.
   const long long chunk = steps_per_launch;
-  long long n_launch = (total + chunk - 1) / chunk;
-  if (n_launch == 0) n_launch = 1;  // run with zero transitions still records row 0
+  std::vector<long long> seg_start, seg_len;
+  std::vector<char> seg_update;
+  {
+    std::vector<long long> wends;
+    if (ns.mass_mode) {
+      const long long lim = n_discard > ns.m_eb ? n_discard - ns.m_eb : 0;
+      for (long long m = 1; m <= total && m <= n_discard; ++m) {
+        if (m <= ns.m_sb || !(m < lim)) continue;  // should_collect
+        if (m >= ns.sched_next || m + 1 >= lim) {  // note_if_window_end
+          ns.sched_next += ns.sched_len;
+          ns.sched_len = ns.sched_len * 2 < 400 ? ns.sched_len * 2 : 400;
+          wends.push_back(m);
+        }
+      }
+    }
+    size_t wi = 0;
+    long long s0 = 0;
+    do {
+      long long n = total - s0 < chunk ? total - s0 : chunk;
+      if (n < 0) n = 0;
+      char upd = 0;
+      if (wi < wends.size() && wends[wi] <= s0 + n) {  // cut at the window end (step m = s0 + n)
+        n = wends[wi] - s0;
+        upd = 1;
+        ++wi;
+      }
+      seg_start.push_back(s0);
+      seg_len.push_back(n);
+      seg_update.push_back(upd);
+      s0 += n;
+    } while (s0 < total);
+    if (seg_update.back()) {  // an update on the last transition still re-finds epsilon
+      seg_start.push_back(total);
+      seg_len.push_back(0);
+      seg_update.push_back(0);
+    }
+  }
+  const long long n_launch = (long long)seg_start.size();
   while ((long long)evs.size() < 2 * n_launch) {
     hipEvent_t ev;
     if (hipEventCreate(&ev) != hipSuccess) {
@@ -471,10 +940,17 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     }
     evs.push_back(ev);
   }
-  long long li = 0;
-  for (long long start = 0; li < n_launch; start += chunk, ++li) {
-    long long nst = total - start < chunk ? total - start : chunk;
-    if (nst < 0) nst = 0;
+  if (ns.mass_mode) {  // RunningCov::reset in init_chain_state (:744-746)
+    hipMemsetAsync(ns.rn, 0, C * sizeof(int), st);
+    hipMemsetAsync(ns.rmean, 0, (size_t)C * D * esz, st);
+    hipMemsetAsync(ns.rm2d, 0, (size_t)C * D * esz, st);
+    if (ns.mass_mode == 2) hipMemsetAsync(ns.rm2, 0, (size_t)C * D * D * esz, st);
+    hipMemsetAsync(ns.updated, 0, C * sizeof(int), st);
+  }
+  int pending_refind = 0;
+  uint64_t refind_step = 0;
+  for (long long li = 0; li < n_launch; ++li) {
+    const long long start = seg_start[li], nst = seg_len[li];
     NutsLaunch a;
     a.q = q;
     a.accepts = accepts;
@@ -499,10 +975,27 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     a.n_steps = (int)nst;
     a.m0 = ns.m + start;
     a.n_discard = n_discard;
-    a.do_init = (start == 0) ? 1 : 0;
+    a.do_init = (start == 0 && li == 0) ? 1 : 0;
     a.t0 = start;
     a.row_shift = row_shift;
     a.n_rows = n_rows_total > 0 ? n_rows_total : 0;
+    if (ns.mass_mode) {
+      a.mass_mode = ns.mass_mode;
+      a.mkind = ns.mkind;
+      a.dinv = ns.dinv;
+      a.dsq = ns.dsq;
+      a.minv = ns.minv;
+      a.mchol = ns.mchol;
+      a.rn = ns.rn;
+      a.rmean = ns.rmean;
+      a.rm2d = ns.rm2d;
+      a.rm2 = ns.rm2;
+      a.updated = ns.updated;
+      a.sb = ns.m_sb;
+      a.eb = ns.m_eb;
+      a.do_refind = pending_refind;
+      a.refind_step = refind_step;
+    }
     if (trk) {
       a.trk = *trk;
       a.trk.n0 = trk->n0 + (unsigned long long)start;
@@ -519,6 +1012,27 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
       return GM_EHIP;
     }
     hipEventRecord(evs[2 * li + 1], st);
+    pending_refind = 0;
+    if (seg_update[li]) {  // maybe_update_mass_matrix for every chain
+      const unsigned blocks = (unsigned)((C + 63) / 64);
+      if (dt == GM_F32)
+        hipLaunchKernelGGL(nuts_mass_update_kernel<float>, dim3(blocks), dim3(64), 0, st, C, D, ns.mass_mode,
+                           ns.m_reg, ns.m_jit, ns.mkind, (float*)ns.dinv, (float*)ns.dsq, (float*)ns.minv,
+                           (float*)ns.mchol, ns.rn, (float*)ns.rmean, (float*)ns.rm2d, (float*)ns.rm2,
+                           ns.updated, (float*)ns.mscratch);
+      else
+        hipLaunchKernelGGL(nuts_mass_update_kernel<double>, dim3(blocks), dim3(64), 0, st, C, D, ns.mass_mode,
+                           ns.m_reg, ns.m_jit, ns.mkind, (double*)ns.dinv, (double*)ns.dsq, (double*)ns.minv,
+                           (double*)ns.mchol, ns.rn, (double*)ns.rmean, (double*)ns.rm2d, (double*)ns.rm2,
+                           ns.updated, (double*)ns.mscratch);
+      hipError_t e2 = hipGetLastError();
+      if (e2 != hipSuccess) {
+        set_error(std::string("mass update launch failed: ") + hipGetErrorString(e2));
+        return GM_EHIP;
+      }
+      pending_refind = 1;
+      refind_step = *step + (uint64_t)(start + nst - 1);
+    }
     if (hook && *hook) {
       const int rc = (*hook)(start + nst);
       if (rc) return rc;

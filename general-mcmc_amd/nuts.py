@@ -6,13 +6,51 @@ run performs n_collect + n_discard - 1 transitions (row 0 is the start when
 n_discard == 0); run_progress performs n_collect + n_discard.
 Every chain runs its own trajectory tree on the GPU (identity mass matrix,
 dual-averaging step size, as NUTS::new configures GenericNUTS).
+NUTS.new_with_mass_matrix adds the warm-up metric adaptation of
+GenericNUTS::new_with_mass_matrix (generic_nuts.rs:33-359, 379-398).
 """
 from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
 
 import numpy as np
 
 from . import _lib
 from ._sampler import Sampler
+
+
+@dataclass
+class NUTSMassMatrixConfig:
+    """NUTSMassMatrixConfig (generic_nuts.rs:43-79): adaptation is "none",
+    "diagonal" or "dense"; the defaults are the reference's Default impl."""
+    adaptation: str = "diagonal"
+    start_buffer: int = 75
+    end_buffer: int = 50
+    initial_window: int = 25
+    regularize: float = 0.05
+    jitter: float = 1e-6
+    dense_max_dim: int = 75
+
+    @classmethod
+    def disabled(cls) -> "NUTSMassMatrixConfig":
+        return cls("none", 0, 0, 0, 0.0, 0.0, 0)
+
+    @property
+    def mode(self) -> int:
+        return {"none": 0, "diagonal": 1, "dense": 2}[self.adaptation.lower()]
+
+
+@dataclass
+class MassMatrix:
+    """The per-chain metric: kind [C] (0 identity, 1 diagonal, 2 dense), the
+    diagonal inverse / sqrt [C, dim], the dense inverse / Cholesky factor
+    [C, dim, dim] (None unless dense adaptation is on)."""
+    kind: np.ndarray
+    diag_inv: np.ndarray
+    diag_sqrt: np.ndarray
+    dense_inv: np.ndarray | None
+    dense_chol: np.ndarray | None
 
 
 class NUTS(Sampler):
@@ -24,6 +62,36 @@ class NUTS(Sampler):
         self.target_accept_p = float(target_accept_p)
         super().__init__(lambda lib: lib.gm_nuts_create, target, initial_positions, dtype,
                          chain_offset, self.target_accept_p, int(max_depth))
+
+    @classmethod
+    def new_with_mass_matrix(cls, target, initial_positions, target_accept_p: float,
+                             mass_config: NUTSMassMatrixConfig, **kw) -> "NUTS":
+        """GenericNUTS::new_with_mass_matrix (generic_nuts.rs:379-398)."""
+        s = cls(target, initial_positions, target_accept_p, **kw)
+        s.set_mass_adaptation(mass_config)
+        return s
+
+    def set_mass_adaptation(self, cfg: NUTSMassMatrixConfig) -> "NUTS":
+        _lib.check(self._lib.gm_nuts_set_mass_adaptation(
+            self._h, cfg.mode, cfg.start_buffer, cfg.end_buffer, cfg.initial_window, cfg.regularize,
+            cfg.jitter, cfg.dense_max_dim))
+        return self
+
+    def mass_matrix(self) -> MassMatrix:
+        mode = C.c_int32()
+        kind = np.zeros(self.n_chains, dtype=np.int32)
+        _lib.check(self._lib.gm_nuts_get_mass(self._h, C.byref(mode), _lib.ptr(kind), None, None, None, None))
+        d = (self.n_chains, self.dim)
+        dinv, dsq = np.zeros(d, dtype=self.dtype), np.zeros(d, dtype=self.dtype)
+        minv = mchol = None
+        if mode.value == 2:
+            minv = np.zeros(d + (self.dim,), dtype=self.dtype)
+            mchol = np.zeros(d + (self.dim,), dtype=self.dtype)
+        if mode.value:
+            _lib.check(self._lib.gm_nuts_get_mass(self._h, None, None, _lib.ptr(dinv), _lib.ptr(dsq),
+                                                  None if minv is None else _lib.ptr(minv),
+                                                  None if mchol is None else _lib.ptr(mchol)))
+        return MassMatrix(kind, dinv, dsq, minv, mchol)
 
     def set_seed(self, seed: int) -> "NUTS":
         """nuts.rs:299-304 / generic_nuts.rs:550-556."""

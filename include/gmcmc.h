@@ -184,6 +184,24 @@ int gm_get_leapfrog_counts(gm_sampler* s, int64_t* out);
  * (generic_nuts.rs:573-582). Pass NULL to skip either. */
 int gm_nuts_get_step_size(gm_sampler* s, double* eps, double* eps_bar);
 
+/* Mass-matrix warm-up, GenericNUTS::new_with_mass_matrix (generic_nuts.rs:
+ * 33-65, 379-398): mode 0 none (NUTS::new), 1 diagonal, 2 dense (falls back
+ * to diagonal when dim > dense_max_dim). During warm-up (m <= n_discard) the
+ * positions inside the window (start_buffer < m < n_discard - end_buffer)
+ * feed a Welford covariance; at each window end (initial_window, doubling
+ * up to 400) the metric becomes (1-regularize)*cov + regularize (diagonal
+ * floored at jitter), the step size is re-found from a probe momentum and
+ * dual averaging restarts (:897-921, 948-997). Resets the metric to identity
+ * and the window schedule to its start; call before the first run. */
+int gm_nuts_set_mass_adaptation(gm_sampler* s, int32_t mode, int64_t start_buffer, int64_t end_buffer,
+                                int64_t initial_window, double regularize, double jitter,
+                                int64_t dense_max_dim);
+/* The current metric: mode, per-chain kind [C] (0 identity, 1 diagonal,
+ * 2 dense), diagonal inverse and sqrt [C][dim], dense inverse and Cholesky
+ * factor [C][dim][dim] (mode 2). Any output may be NULL. */
+int gm_nuts_get_mass(gm_sampler* s, int32_t* mode, int32_t* kind, void* dinv, void* dsqrt, void* minv,
+                     void* mchol);
+
 /* Lane layout the kernels use for this sampler: `lanes` lanes cooperate on
  * one chain, each holding `elems` consecutive coordinates. Per-chain sums
  * (kinetic energy, log-density) are reduced lane-sequentially then by an xor

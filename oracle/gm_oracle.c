@@ -19,7 +19,8 @@
 
 enum {
   TAG_INIT = 1, TAG_MOM = 2, TAG_ACC = 3, TAG_MH_PROP = 4, TAG_MH_ACC = 5, TAG_NUTS_MOM = 6,
-  TAG_NUTS_EXP = 7, TAG_NUTS_DIR = 8, TAG_NUTS_TOP = 9, TAG_NUTS_MRG = 10, TAG_NUTS_INIT = 11
+  TAG_NUTS_EXP = 7, TAG_NUTS_DIR = 8, TAG_NUTS_TOP = 9, TAG_NUTS_MRG = 10, TAG_NUTS_INIT = 11,
+  TAG_NUTS_PROBE = 12 /* probe momentum after a mass-matrix update (generic_nuts.rs:905-909) */
 };
 
 /* ===================== Part 1: RNG spec ===================== */
@@ -329,6 +330,51 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #undef T
 #undef SFX
 
+/* ---- mass-matrix warm-up: state init and the reference's unit tests ---- */
+void or_mass_state_init(const or_mass_cfg* cfg, int64_t C, int D, int dtype_is_f64, or_mass_state* st) {
+  (void)D;
+  (void)dtype_is_f64;
+  const int64_t sb = cfg->start_buffer > 1 ? cfg->start_buffer : 1;   /* MassMatrixWarmup::new */
+  const int64_t wl = cfg->initial_window > 10 ? cfg->initial_window : 10;
+  st->sched[0] = sb + wl;
+  st->sched[1] = wl;
+  for (int64_t c = 0; c < C; ++c) st->kind[c] = 0;  /* MassMatrix::identity */
+}
+
+int or_mass_diag_kat(const double* var, int D, double jitter, const double* p, double* ke,
+                     double* inv_mul_out) {
+  double inv[64], sq[64];
+  if (D > 64) return 1;
+  diag_from_var_d(var, D, jitter, inv, sq);
+  double q = 0.0;  /* MassMatrix::kinetic, diagonal (generic_nuts.rs:239-245) */
+  for (int i = 0; i < D; ++i) q = q + p[i] * p[i] * inv[i];
+  *ke = 0.5 * q;
+  mass_d M = {1, inv, sq, NULL};
+  inv_mul_d(&M, p, inv_mul_out, D);
+  return 0;
+}
+
+int or_mass_dense_kat(const double* cov, int D, double jitter, const double* p, double* inv_mul_out) {
+  double inv[64 * 64], chol[64 * 64];
+  if (D > 64) return 1;
+  if (!dense_from_cov_d(cov, D, jitter, inv, chol)) return 2;
+  mass_d M = {2, inv, NULL, chol};
+  inv_mul_d(&M, p, inv_mul_out, D);
+  return 0;
+}
+
+int or_mass_warmup_diag_kat(const double* xs, int n, int D, double reg, double jitter, double* inv,
+                            double* sqrt_out) {
+  double mean[64], m2d[64], delta[64];
+  if (D > 64) return 1;
+  running_d r = {0, mean, m2d, NULL, delta};
+  running_reset_d(&r, D, 0);
+  for (int k = 0; k < n; ++k) running_update_d(&r, xs + (size_t)k * D, D, 0);
+  or_mass_cfg cfg = {1, 1, 1, 4, reg, jitter};
+  mass_d M = {0, inv, sqrt_out, NULL};
+  return maybe_update_d(&cfg, &r, D, &M, inv, sqrt_out) ? 0 : 2;
+}
+
 /* ===================== Part 3: diagnostics (stats.rs, f32) ===================== */
 
 /* ndarray-style contiguous f32 sum: eight interleaved accumulators, folded. */
@@ -592,8 +638,10 @@ double or_find_reasonable_epsilon_d(const or_target* t, int lanes, int elems, co
   memset(&cx, 0, sizeof(cx));
   cx.t = t; cx.lanes = lanes; cx.elems = elems; cx.D = t->dim;
   cx.tmpv = (double*)malloc(sizeof(double) * t->dim);
+  cx.tmpv2 = (double*)malloc(sizeof(double) * t->dim);
   double e = find_eps_d(&cx, q, p);
   free(cx.tmpv);
+  free(cx.tmpv2);
   return e;
 }
 
@@ -608,6 +656,7 @@ void or_build_tree_d(const or_target* t, int lanes, int elems, const double* q, 
   cx.seed = seed; cx.cid = chain; cx.step = step;
   for (int k = 0; k < 32; ++k) tree_alloc_d(&cx.ws[k], D);
   cx.tmpv = (double*)malloc(sizeof(double) * D);
+  cx.tmpv2 = (double*)malloc(sizeof(double) * D);
   tree_d out;
   tree_alloc_d(&out, D);
   build_tree_d(&cx, q, p, g, logu, v, j, eps, joint0, &out);
@@ -621,4 +670,5 @@ void or_build_tree_d(const or_target* t, int lanes, int elems, const double* q, 
   for (int k = 0; k < 32; ++k) free(cx.ws[k].qm);
   free(out.qm);
   free(cx.tmpv);
+  free(cx.tmpv2);
 }

@@ -87,6 +87,45 @@ int or_nuts_run_f(const or_target* t, int lanes, int elems, int64_t C, int D, fl
                   int max_depth, uint64_t seed, uint64_t init_step, uint32_t chain_offset,
                   int64_t n_collect, int64_t n_discard, int progress, float* samples,
                   int64_t* accepts, int64_t* n_leapfrog, int threads);
+/* ---- NUTS mass-matrix warmup (generic_nuts.rs:33-359, 897-921) ----
+ * GenericNUTS::new_with_mass_matrix: Welford windows during warm-up, the
+ * diagonal or dense metric, the probe + find_reasonable_epsilon re-start
+ * after each update. The state persists across runs. */
+typedef struct or_mass_cfg {
+  int mode; /* 0 none, 1 diagonal, 2 dense (dense_max_dim already applied) */
+  int64_t start_buffer, end_buffer, initial_window;
+  double regularize, jitter;
+} or_mass_cfg;
+typedef struct or_mass_state {
+  int32_t* kind;     /* [C]: 0 identity, 1 diagonal, 2 dense */
+  void* dinv;        /* [C][D] T: diagonal inverse */
+  void* dsqrt;       /* [C][D] T: diagonal sqrt */
+  void* minv;        /* [C][D][D] T: dense inverse (mode 2) */
+  void* mchol;       /* [C][D][D] T: dense Cholesky factor (mode 2) */
+  int64_t sched[2];  /* next_window_end, window_len (MassMatrixWarmup::new, :141-151) */
+} or_mass_state;
+/* MassMatrixWarmup::new's schedule and identity for every chain */
+void or_mass_state_init(const or_mass_cfg* cfg, int64_t C, int D, int dtype_is_f64, or_mass_state* st);
+int or_nuts_mass_run_d(const or_target* t, int lanes, int elems, int64_t C, int D, double* q,
+                       double* eps, double* eps_bar, double* h_bar, double* mu, double target_accept,
+                       int max_depth, uint64_t seed, uint64_t init_step, uint32_t chain_offset,
+                       int64_t n_collect, int64_t n_discard, int progress, double* samples,
+                       int64_t* accepts, int64_t* n_leapfrog, const or_mass_cfg* cfg,
+                       or_mass_state* ms, int threads);
+int or_nuts_mass_run_f(const or_target* t, int lanes, int elems, int64_t C, int D, float* q,
+                       float* eps, float* eps_bar, float* h_bar, float* mu, double target_accept,
+                       int max_depth, uint64_t seed, uint64_t init_step, uint32_t chain_offset,
+                       int64_t n_collect, int64_t n_discard, int progress, float* samples,
+                       int64_t* accepts, int64_t* n_leapfrog, const or_mass_cfg* cfg,
+                       or_mass_state* ms, int threads);
+/* the reference's MassMatrix unit tests (generic_nuts.rs:1427-1489):
+ * diagonal_from_var -> kinetic / inv_mul; dense_from_cov -> inv_mul;
+ * RunningCov + maybe_update_mass_matrix (diagonal). Return 0 on success. */
+int or_mass_diag_kat(const double* var, int D, double jitter, const double* p, double* ke,
+                     double* inv_mul_out);
+int or_mass_dense_kat(const double* cov, int D, double jitter, const double* p, double* inv_mul_out);
+int or_mass_warmup_diag_kat(const double* xs, int n, int D, double reg, double jitter, double* inv,
+                            double* sqrt_out);
 double or_find_reasonable_epsilon_d(const or_target* t, int lanes, int elems, const double* q,
                                     const double* p);
 /* build_tree (generic_nuts.rs:1105-1341), identity mass; out vectors [dim]:

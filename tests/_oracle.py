@@ -59,6 +59,14 @@ def load():
         getattr(lib, f"or_nuts_run_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _vp, _vp,
                                                        _vp, _vp, _dbl, _int, _u64, _u64, _u32,
                                                        _i64, _i64, _int, _vp, _vp, _vp, _int]
+    for sfx in ("d", "f"):
+        getattr(lib, f"or_nuts_mass_run_{sfx}").argtypes = [
+            tp, _int, _int, _i64, _int, _vp, _vp, _vp, _vp, _vp, _dbl, _int, _u64, _u64, _u32, _i64,
+            _i64, _int, _vp, _vp, _vp, C.POINTER(or_mass_cfg), C.POINTER(or_mass_state), _int]
+    lib.or_mass_state_init.argtypes = [C.POINTER(or_mass_cfg), _i64, _int, _int, C.POINTER(or_mass_state)]
+    lib.or_mass_diag_kat.argtypes = [_vp, _int, _dbl, _vp, _vp, _vp]
+    lib.or_mass_dense_kat.argtypes = [_vp, _int, _dbl, _vp, _vp]
+    lib.or_mass_warmup_diag_kat.argtypes = [_vp, _int, _int, _dbl, _dbl, _vp, _vp]
     lib.or_philox.argtypes = [C.POINTER(C.c_uint32)] * 3
     lib.or_find_reasonable_epsilon_d.restype = _dbl
     lib.or_find_reasonable_epsilon_d.argtypes = [tp, _int, _int, _vp, _vp]
@@ -75,6 +83,34 @@ def load():
     lib.or_collect_rhat.argtypes = [_i64, _i64, _u64, _vp, _vp, _vp]
     _lib = lib
     return Oracle(lib)
+
+
+class or_mass_cfg(C.Structure):
+    _fields_ = [("mode", C.c_int), ("start_buffer", C.c_int64), ("end_buffer", C.c_int64),
+                ("initial_window", C.c_int64), ("regularize", C.c_double), ("jitter", C.c_double)]
+
+
+class or_mass_state(C.Structure):
+    _fields_ = [("kind", C.c_void_p), ("dinv", C.c_void_p), ("dsqrt", C.c_void_p),
+                ("minv", C.c_void_p), ("mchol", C.c_void_p), ("sched", C.c_int64 * 2)]
+
+
+class NutsMass:
+    """Host arrays of the oracle's per-chain mass state (or_mass_state)."""
+
+    def __init__(self, lib, mode, C_, D, dtype, start_buffer=75, end_buffer=50, initial_window=25,
+                 regularize=0.05, jitter=1e-6):
+        self.cfg = or_mass_cfg(mode, start_buffer, end_buffer, initial_window, regularize, jitter)
+        self.kind = np.zeros(C_, dtype=np.int32)
+        self.dinv = np.zeros((C_, D), dtype=dtype)
+        self.dsqrt = np.zeros((C_, D), dtype=dtype)
+        nd = D if mode == 2 else 0
+        self.minv = np.zeros((C_, nd, nd), dtype=dtype)
+        self.mchol = np.zeros((C_, nd, nd), dtype=dtype)
+        self.st = or_mass_state(_p(self.kind).value, _p(self.dinv).value, _p(self.dsqrt).value,
+                                _p(self.minv).value if nd else None, _p(self.mchol).value if nd else None)
+        lib.or_mass_state_init(C.byref(self.cfg), C_, D, int(np.dtype(dtype) == np.float64),
+                               C.byref(self.st))
 
 
 def _p(a):
@@ -206,6 +242,27 @@ class Oracle:
         r = np.empty(p, dtype=np.float32)
         self.lib.or_mct_rhat(_p(s), ns, c, p, _p(r))
         return r
+
+    def nuts_mass(self, mode, C_, D, dtype, **cfg):
+        return NutsMass(self.lib, mode, C_, D, dtype, **cfg)
+
+    def nuts_mass_run(self, target: Target, q, state, mass: NutsMass, target_accept, max_depth, seed,
+                      init_step, n_collect, n_discard, progress, lanes, elems, chain_offset=0,
+                      threads=8):
+        """or_nuts_run with mass-matrix warm-up (GenericNUTS::new_with_mass_matrix)."""
+        q = np.array(q, copy=True, order="C")
+        C_, D = q.shape
+        samples = np.zeros((n_collect, C_, D), dtype=q.dtype)
+        acc = np.zeros(C_, dtype=np.int64)
+        nlf = np.zeros(C_, dtype=np.int64)
+        t = target.struct()
+        rc = getattr(self.lib, f"or_nuts_mass_run_{_sfx(q.dtype)}")(
+            C.byref(t), lanes, elems, C_, D, _p(q), _p(state["eps"]), _p(state["eps_bar"]),
+            _p(state["h_bar"]), _p(state["mu"]), target_accept, max_depth, seed, init_step,
+            chain_offset, n_collect, n_discard, int(progress), _p(samples), _p(acc), _p(nlf),
+            C.byref(mass.cfg), C.byref(mass.st), threads)
+        assert rc == 0
+        return q, samples, acc, nlf
 
     def mct_p_accept(self, steps):
         """MultiChainTracker acceptance EMA after stepping [nsteps, C, P]."""

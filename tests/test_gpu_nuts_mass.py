@@ -1,0 +1,122 @@
+"""NUTS with mass-matrix warm-up (GenericNUTS::new_with_mass_matrix,
+generic_nuts.rs:33-359, 379-398, 897-921, 948-997) on the GPU, bit-exact
+against the oracle's restatement driven by the same Philox streams:
+samples, the learned metric, the step sizes; across two runs (metric and
+window schedule persist), and with run_progress semantics."""
+import numpy as np
+import pytest
+
+from tests._oracle import Target
+
+pytestmark = pytest.mark.gpu
+
+SMALL = dict(start_buffer=5, end_buffer=5, initial_window=10)
+
+
+def _gauss(gm, cov, mean=None):
+    cov = np.asarray(cov, dtype=np.float64)
+    mean = np.zeros(len(cov)) if mean is None else np.asarray(mean, dtype=np.float64)
+    return gm.DenseGaussian(mean, cov)
+
+
+def _check_run(gm, oracle, t, x0, dtype, mode, runs, progress=False, **cfg):
+    C_, D = x0.shape
+    adapt = {1: "diagonal", 2: "dense"}[mode]
+    mc = gm.NUTSMassMatrixConfig(adapt, **{**dict(regularize=0.05, jitter=1e-6, dense_max_dim=75), **cfg})
+    s = gm.NUTS.new_with_mass_matrix(t, x0, 0.8, mc, dtype=dtype).set_seed(11)
+    lanes, elems = s.layout()
+    ot = Target.from_product(t, D)
+    st = oracle.nuts_state(C_, dtype)
+    om = oracle.nuts_mass(mode, C_, D, dtype, **{k: v for k, v in cfg.items() if k != "dense_max_dim"})
+    q = np.array(x0, dtype=dtype)
+    init_step = 0
+    for nc, nd in runs:
+        if progress:
+            out, _ = s.run_progress(nc, nd)
+        else:
+            out = s.run(nc, nd)
+        q, smp, _, _ = oracle.nuts_mass_run(ot, q, st, om, 0.8, 10, 11, init_step, nc, nd, progress,
+                                            lanes, elems)
+        np.testing.assert_array_equal(out, smp.transpose(1, 0, 2))
+        total = nc + nd if progress else nc + nd - 1
+        init_step += total + 1
+        m = s.mass_matrix()
+        np.testing.assert_array_equal(m.kind, om.kind)
+        np.testing.assert_array_equal(m.diag_inv[om.kind == 1], om.dinv[om.kind == 1])
+        np.testing.assert_array_equal(m.diag_sqrt[om.kind == 1], om.dsqrt[om.kind == 1])
+        if mode == 2:
+            np.testing.assert_array_equal(m.dense_inv[om.kind == 2], om.minv[om.kind == 2])
+            np.testing.assert_array_equal(m.dense_chol[om.kind == 2], om.mchol[om.kind == 2])
+        eps, bar = s.step_sizes()
+        np.testing.assert_array_equal(eps.astype(dtype), st["eps"])
+        np.testing.assert_array_equal(bar.astype(dtype), st["eps_bar"])
+    return s, om
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_diag_warmup_bitexact(gm, oracle, dtype):
+    t = _gauss(gm, np.diag([0.04, 1.0, 4.0, 0.5]))
+    x0 = gm.init_with_seed(24, 4, 3, dtype)
+    s, om = _check_run(gm, oracle, t, x0, dtype, 1, [(20, 60), (15, 40)], **SMALL)
+    assert np.all(om.kind == 1)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_dense_warmup_bitexact(gm, oracle, dtype):
+    cov = np.array([[2.0, 0.9, 0.0], [0.9, 1.0, 0.3], [0.0, 0.3, 0.5]])
+    t = _gauss(gm, cov, [0.5, -1.0, 0.0])
+    x0 = gm.init_with_seed(16, 3, 4, dtype)
+    s, om = _check_run(gm, oracle, t, x0, dtype, 2, [(12, 70), (10, 45)], **SMALL)
+    assert np.all(om.kind >= 1)
+
+
+def test_dense_warmup_wide_layout(gm, oracle):
+    """D = 40 (two coordinates per lane at the default layout? no: 64 lanes x 1)
+    and D = 70 (64 lanes x 2): the lane broadcasts of the dense products."""
+    rng = np.random.default_rng(9)
+    for D in (40, 70):
+        a = rng.standard_normal((D, D))
+        cov = a @ a.T / D + 0.5 * np.eye(D)
+        t = _gauss(gm, cov)
+        x0 = gm.init_with_seed(6, D, 5, np.float64)
+        _check_run(gm, oracle, t, x0, np.float64, 2, [(6, 40)], start_buffer=4, end_buffer=4,
+                   initial_window=10)
+
+
+def test_progress_semantics_with_mass(gm, oracle):
+    t = _gauss(gm, np.diag([0.25, 2.0, 1.0]))
+    x0 = gm.init_with_seed(10, 3, 6, np.float64)
+    _check_run(gm, oracle, t, x0, np.float64, 1, [(10, 50)], progress=True, **SMALL)
+
+
+def test_dense_falls_back_to_diagonal_above_max_dim(gm):
+    t = gm.IsotropicGaussian(1.0)
+    s = gm.NUTS.new_with_mass_matrix(t, gm.init_det(4, 6), 0.8,
+                                     gm.NUTSMassMatrixConfig("dense", dense_max_dim=5, **SMALL))
+    s.run(5, 40)
+    m = s.mass_matrix()
+    assert m.dense_inv is None and np.all(m.kind == 1)
+
+
+def test_default_schedule_recovers_scales(gm, oracle):
+    """The reference defaults (75 / 25 / 50, windows ending at m = 100, 150,
+    250, 450, 549 for 600 warm-up steps): chains spot-checked bit-exactly
+    against the oracle, and the diagonal metric tracks 0.95 * var + 0.05
+    (generic_nuts.rs:962-964) within the noise of a ~100-draw last window."""
+    std = np.array([0.3, 1.0, 2.0])
+    t = _gauss(gm, np.diag(std ** 2))
+    x0 = gm.init_with_seed(256, 3, 8)
+    s = gm.NUTS.new_with_mass_matrix(t, x0, 0.8, gm.NUTSMassMatrixConfig()).set_seed(0)
+    out = s.run(50, 600)
+    m = s.mass_matrix()
+    assert np.all(m.kind == 1)
+    var = 1.0 / m.diag_inv
+    np.testing.assert_allclose(np.median(var, axis=0), 0.95 * std ** 2 + 0.05, rtol=0.5)
+    lanes, elems = s.layout()
+    for c in (0, 131, 255):
+        st = oracle.nuts_state(1, np.float64)
+        om = oracle.nuts_mass(1, 1, 3, np.float64)
+        _, smp, _, _ = oracle.nuts_mass_run(Target.from_product(t, 3), x0[c:c + 1], st, om, 0.8, 10, 0, 0,
+                                            50, 600, False, lanes, elems, chain_offset=c)
+        np.testing.assert_array_equal(out[c], smp[:, 0, :])
+        np.testing.assert_array_equal(m.diag_inv[c], om.dinv[0])
