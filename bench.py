@@ -117,6 +117,8 @@ def main():
         except Exception:
             traffic = None
 
+    copy_gbs = copy_ceiling(lib) if rank == 0 else None
+
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
         cpu = cpu_baseline(gm, a, dtype, x0, lanes, elems)
@@ -150,7 +152,8 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "valu": {"achieved_tflops": achieved_tflops,
                                   "peak_tflops": VALU_F32_PEAK_TFLOPS,
-                                  "frac": achieved_tflops / VALU_F32_PEAK_TFLOPS}},
+                                  "frac": achieved_tflops / VALU_F32_PEAK_TFLOPS},
+                         "copy_ceiling_gbs": copy_gbs},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -158,6 +161,41 @@ def main():
         comm.close()
     sampler.close()
     cp.close()
+
+
+def copy_ceiling(lib, nbytes=1 << 30, reps=5):
+    """Empirical HBM ceiling on this box: a 1 GiB
+    device-to-device copy, read + write bytes over the median time."""
+    import ctypes as C
+    from general_mcmc_amd import _lib
+    src, dst = C.c_void_p(), C.c_void_p()
+    try:
+        _lib.check(lib.gm_malloc(C.byref(src), nbytes))
+        _lib.check(lib.gm_malloc(C.byref(dst), nbytes))
+        ts = []
+        for _ in range(reps + 1):
+            _lib.check(lib.gm_device_synchronize())
+            t0 = time.perf_counter()
+            _lib.check(lib.gm_memcpy_dtod(dst, src, nbytes))
+            _lib.check(lib.gm_device_synchronize())
+            ts.append(time.perf_counter() - t0)
+        return 2 * nbytes / float(np.median(ts[1:])) / 1e9
+    except Exception:
+        return None
+    finally:
+        for p in (src, dst):
+            if p.value:
+                lib.gm_free(p)
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def cpu_baseline(gm, a, dtype, x0, lanes, elems):
@@ -176,10 +214,18 @@ def cpu_baseline(gm, a, dtype, x0, lanes, elems):
     t0 = time.perf_counter()
     ora.hmc_run(t, q, a.eps, a.leapfrog, 42, 1, steps, steps, lanes, elems, threads=threads)
     dt = time.perf_counter() - t0
+    # one thread on a slice of the chains (the reference's per-core rate)
+    n1 = max(1, x0.shape[0] // threads)
+    q1 = np.array(x0[:n1], copy=True)
+    t0 = time.perf_counter()
+    ora.hmc_run(t, q1, a.eps, a.leapfrog, 42, 1, steps, steps, lanes, elems, threads=1)
+    dt1 = time.perf_counter() - t0
     return {"value": x0.shape[0] * a.leapfrog * steps / dt, "unit": "chain-leapfrog steps/s",
             "cores": threads, "kind": "port",
             "sample": f"{x0.shape[0]} chains x {steps} transitions x {a.leapfrog} leapfrogs "
-                      f"(oracle/gm_oracle.c, {threads} threads, {dt:.1f}s)"}
+                      f"(oracle/gm_oracle.c, {threads} threads, {dt:.1f}s)",
+            "one_thread_value": n1 * a.leapfrog * steps / dt1,
+            "host": {"cpu_model": _cpu_model(), "nproc": os.cpu_count()}}
 
 
 if __name__ == "__main__":
