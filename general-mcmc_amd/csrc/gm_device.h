@@ -139,6 +139,9 @@ template <class T> struct RosenbrockT {
       const int i = lane * E + e;
       r.ms[e] = lane_mask<T>(i <= D - 2);
       r.mp[e] = lane_mask<T>((i >= 1) & (i <= D - 1));
+      r.b4m[e] = (i <= D - 2) ? b4 : (T)0;
+      r.c2m[e] = (i <= D - 2) ? (T)2 : (T)0;
+      r.b2m[e] = ((i >= 1) & (i <= D - 1)) ? b2 : (T)0;
     }
     return r;
   }
@@ -146,9 +149,45 @@ template <class T> struct RosenbrockT {
 template <class T, int E> struct RosenbrockLane {
   T a, b, b2, b4;
   typename MaskOf<T>::type ms[E], mp[E];  // [i <= D-2], [1 <= i <= D-1]
+  T b4m[E], c2m[E], b2m[E];               // 4b, 2, 2b where those masks hold, else 0
   template <int LPC, int E_, bool LOGP>
   __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int) const {
     static_assert(E_ == E, "layout mismatch");
+    if constexpr (LPC == 64) {
+      // One chain per wave: the lane shifts read 0 beyond the wave and the
+      // padding coordinates are 0, so a boundary lane can only see finite
+      // values of its own chain. The [.] factors are then applied by
+      // multiplying with per-lane constants that are 0 where the term is
+      // absent (the engine's canonical form for 64-lane groups; the oracle
+      // mirrors it), and (x_{i-1})^2 is shifted in from the lane that
+      // computed it, so t_{i-1} is one DPP-fed subtract.
+      T xx[E], t[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) xx[e] = x[e] * x[e];
+      const T nx = from_next<LPC>(x[0]);
+      const T pxx = from_prev<LPC>(xx[E - 1]);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const T xn = (e + 1 < E) ? x[(e + 1 < E) ? e + 1 : e] : nx;
+        t[e] = xn - xx[e];
+      }
+      const T tp = x[0] - pxx;
+      T part = (T)0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const T tprev = (e > 0) ? t[(e > 0) ? e - 1 : 0] : tp;
+        const T am = a - x[e];
+        const T A = (b4m[e] * x[e]) * t[e] + c2m[e] * am;
+        const T B = b2m[e] * tprev;
+        g[e] = A - B;
+        if (LOGP) {
+          const T s = keep(b * (t[e] * t[e]) + am * am, ms[e]);
+          part = (e == 0) ? s : part + s;
+        }
+      }
+      if (LOGP) return -group_sum<LPC>(part);
+      return (T)0;
+    }
     T t[E];
     // Both lane shifts read x only: t_{i-1} for a group's first slot is
     // recomputed from x_{i-1} (the operands lane i-1 uses, so the same bits)

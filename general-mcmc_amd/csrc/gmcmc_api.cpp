@@ -233,6 +233,10 @@ int gm_device_count(int* count) {
 
 int gm_set_device(int device) {
   GM_HIP(hipSetDevice(device));
+  // GM_SYNC_SPIN=1: host waits spin instead of yielding (lower completion
+  // latency for short synchronous runs, at the cost of a busy host core)
+  const char* spin = getenv("GM_SYNC_SPIN");
+  if (spin && atoi(spin) == 1) hipSetDeviceFlags(hipDeviceScheduleSpin);
   return GM_OK;
 }
 
