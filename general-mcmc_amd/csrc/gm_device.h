@@ -69,6 +69,17 @@ __device__ __forceinline__ double lane63(double v) {
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
+// value of lane k (wave-uniform result)
+__device__ __forceinline__ float lane_k(float v, int k) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
+}
+__device__ __forceinline__ double lane_k(double v, int k) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, k);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), k);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
 template <int LPC, class T> __device__ __forceinline__ T group_sum(T v) {
   if constexpr (LPC >= 2) v = v + dpp<DPP_QUAD_XOR1>(v);
   if constexpr (LPC >= 4) v = v + dpp<DPP_QUAD_XOR2>(v);

@@ -45,6 +45,7 @@ struct HmcLaunch {
   int collect_from = 0;         // steps s >= collect_from are stored ...
   long long sample_row0 = 0;    // ... at row sample_row0 + (s - collect_from)
   int lf_unroll = 1;            // leapfrog loop unroll (1 or 4; same results)
+  int stagger = 1;              // per-wave staggered prefetch of the draw blocks (same results)
 };
 hipError_t launch_hmc(gm_dtype dt, const TargetDev& tg, const Layout& lay, const HmcLaunch& a,
                       hipStream_t st);

@@ -537,6 +537,10 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
       a.collect_from = (int)cf;
       a.sample_row0 = row0;
       a.lf_unroll = hmc_lf_unroll((s->C * s->lay.lanes + 63) / 64);
+      {
+        const char* v = getenv("GM_HMC_STAGGER");  // measurement knob
+        a.stagger = v ? (atoi(v) != 0) : 1;
+      }
       e = launch_hmc(s->dt, s->tg, s->lay, a, s->stream);
     } else {
       MhLaunch a;

@@ -45,52 +45,88 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
   T lp = tg.template eval<LPC, E, true>(q, g, lane);
   long long acc = 0;
   constexpr int S = Blk<T>::S;  // one Philox block serves S transitions
-  T zs[E][S];                   // momentum draws of the current block, front = this step
-  T kes[S];                     // their kinetic energies
-  T lus[S];                     // ln u of the accept uniforms
+  // Draw blocks: A = the current block (front = this step), B = the next
+  // one, prefetched. Each wave prefetches on the step whose index matches its
+  // wave phase, so the waves of a SIMD are not all in the Philox/Box-Muller
+  // chain at once and the leapfrogs of the others hide its latency.
+  T zsA[E][S], kesA[S], lusA[S];
+  T zsB[E][S], kesB[S], lusB[S];
+  bool hasB = false;
+  const int phase = a.stagger ? (int)((gtid >> 6) % S) : -1;  // wave index mod S (wave-uniform)
+  // the momenta of block blk, their S kinetic energies (S independent
+  // reductions) and the S accept log-uniforms
+  auto fill = [&](T (&zs)[E][S], T (&kes)[S], T (&lus)[S], uint64_t blk) __attribute__((always_inline)) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      normals_of(draw_block(a.seed, cid, blk, TAG_MOM, (uint32_t)i), zs[e]);
+#pragma unroll
+      for (int k = 0; k < S; ++k) zs[e][k] = (i < D) ? zs[e][k] : (T)0;
+    }
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+      T kp = (T)0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const T sq = zs[e][k] * zs[e][k];
+        kp = (e == 0) ? sq : kp + sq;
+      }
+      kes[k] = group_sum<LPC>(kp) * (T)0.5;  // 2. kinetic energy
+    }
+    T us[S];
+    uniforms_of(draw_block(a.seed, ucid, blk, TAG_ACC, 0u), us);
+    if constexpr (LPC == 64) {
+      // the S logs of wave-uniform inputs: lane k evaluates ln u_k, one
+      // VALU pass for all S, then each value is read back as a scalar
+      T um = us[0];
+#pragma unroll
+      for (int k = 1; k < S; ++k) um = ((lane & (S - 1)) == k) ? us[k] : um;
+      const T lm = glog_unif(um);
+#pragma unroll
+      for (int k = 0; k < S; ++k) lus[k] = lane_k(lm, k);
+    } else {
+#pragma unroll
+      for (int k = 0; k < S; ++k) lus[k] = glog_unif(us[k]);
+    }
+  };
+  const uint64_t st_end = a.step0 + (uint64_t)a.n_steps;
 
   for (int s = 0; s < a.n_steps; ++s) {
     const uint64_t st = a.step0 + (uint64_t)s;
-    if (s == 0 || st % S == 0) {
-      // Refill: S momentum vectors, their S kinetic energies (S independent
-      // reductions) and the S accept log-uniforms, all off the per-step path.
+    const int k0 = (int)(st % S);
+    if (s == 0 || k0 == 0) {
+      if (s > 0 && hasB) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int i = lane * E + e;
-        normals_of(draw_block(a.seed, cid, st / S, TAG_MOM, (uint32_t)i), zs[e]);
+        for (int k = 0; k < S; ++k) {
 #pragma unroll
-        for (int k = 0; k < S; ++k) zs[e][k] = (i < D) ? zs[e][k] : (T)0;
-      }
-#pragma unroll
-      for (int k = 0; k < S; ++k) {
-        T kp = (T)0;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const T sq = zs[e][k] * zs[e][k];
-          kp = (e == 0) ? sq : kp + sq;
+          for (int e = 0; e < E; ++e) zsA[e][k] = zsB[e][k];
+          kesA[k] = kesB[k];
+          lusA[k] = lusB[k];
         }
-        kes[k] = group_sum<LPC>(kp) * (T)0.5;  // 2. kinetic energy
+      } else {
+        fill(zsA, kesA, lusA, st / S);
+#pragma unroll
+        for (int e = 0; e < E; ++e) skip_front(zsA[e], k0);
+        skip_front(kesA, k0);
+        skip_front(lusA, k0);
       }
-      T us[S];
-      uniforms_of(draw_block(a.seed, ucid, st / S, TAG_ACC, 0u), us);
-#pragma unroll
-      for (int k = 0; k < S; ++k) lus[k] = glog_unif(us[k]);
-      const int k0 = (int)(st % S);
-#pragma unroll
-      for (int e = 0; e < E; ++e) skip_front(zs[e], k0);
-      skip_front(kes, k0);
-      skip_front(lus, k0);
+      hasB = false;
     }
     // 1. momentum ~ N(0, I) and its kinetic energy: front of the block
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      p[e] = zs[e][0];
-      shift_front(zs[e]);
+      p[e] = zsA[e][0];
+      shift_front(zsA[e]);
     }
-    const T ke0 = kes[0];
-    const T lnu = lus[0];
-    shift_front(kes);
-    shift_front(lus);
+    const T ke0 = kesA[0];
+    const T lnu = lusA[0];
+    shift_front(kesA);
+    shift_front(lusA);
+    // prefetch the next block (if this launch reaches it)
+    if (!hasB && k0 == phase && st - (uint64_t)k0 + S < st_end) {
+      fill(zsB, kesB, lusB, st / S + 1);
+      hasB = true;
+    }
     // 4. proposal buffers
 #pragma unroll
     for (int e = 0; e < E; ++e) {

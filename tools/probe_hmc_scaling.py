@@ -21,10 +21,11 @@ for kind, L, C, D in cases:
     s.run_positions(0, 8)
     samplers.append((kind, L, C, D, s))
 res = {}
-unrolls = [u for u in os.environ.get("PROBE_UNROLLS", "1").split(",")]
+knob = os.environ.get("PROBE_KNOB", "GM_HMC_UNROLL")
+unrolls = [u for u in os.environ.get("PROBE_VALUES", os.environ.get("PROBE_UNROLLS", "1")).split(",")]
 for r in range(5):
     for u in unrolls:
-        os.environ["GM_HMC_UNROLL"] = u
+        os.environ[knob] = u
         for kind, L, C, D, s in samplers:
             n_steps = 400 if kind == "N400" else 40
             s.run_positions(n_steps, 0)
