@@ -142,6 +142,7 @@ template <class T> struct RosenbrockT {
   T a, b, b2, b4;  // b2 = 2b, b4 = 4b (rounded once, host side)
   int D;
   // per-lane view with the coordinate masks computed once per kernel
+  template <int LPC, int E> __host__ __device__ size_t lds_bytes() const { return 0; }
   template <int LPC, int E> __device__ __forceinline__ RosenbrockLane<T, E> bind(int lane) const {
     RosenbrockLane<T, E> r;
     r.a = a; r.b = b; r.b2 = b2; r.b4 = b4;
@@ -234,6 +235,7 @@ template <class T, int E> struct RosenbrockLane {
 template <class T> struct IsoGaussT {
   T var;  // std*std
   int D;
+  template <int LPC, int E> __host__ __device__ size_t lds_bytes() const { return 0; }
   template <int LPC, int E> __device__ __forceinline__ IsoGaussT bind(int) const { return *this; }
   template <int LPC, int E, bool LOGP>
   __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int lane) const {
@@ -255,34 +257,120 @@ template <class T> struct IsoGaussT {
 // Dense Gaussian (DiffableGaussian2D generalised, distributions.rs:257-292):
 //   d = x - mu; w_k = sum_j P_kj d_j (j ascending); logp = nc - 0.5*sum_k w_k d_k;
 //   g = -w   (= -0.5 (P + P^T) d for symmetric P, the autodiff result)
+//
+// The precision matrix is stored transposed (prec[j*D + i] = P_ij) so that
+// lane i's column-j reads are consecutive across the chain's lanes. When it
+// fits (use_lds, decided per layout by the launcher) bind() stages it once per
+// block into LDS with a row stride of S = LPC*E (zero columns for i >= D, so
+// no lane needs a bounds test), and each evaluation publishes d in a per-group
+// LDS slot from which coordinate j is read as a broadcast: per column one LDS
+// read of P and one broadcast read of d_j, no shuffles, no global loads.
+extern __shared__ __attribute__((aligned(16))) unsigned char gm_dyn_lds[];
+
+template <class T, int LPC, int E> struct GaussLane;
 template <class T> struct GaussT {
   const T* mu;    // [D] device
-  const T* prec;  // [D*D] device row-major
+  const T* prec;  // [D*D] device, transposed: prec[j*D + i] = P_ij
   T nc;
   int D;
-  template <int LPC, int E> __device__ __forceinline__ GaussT bind(int) const { return *this; }
-  template <int LPC, int E, bool LOGP>
+  int use_lds = 0;
+  // dynamic LDS bytes a 256-thread block needs for layout (LPC, E)
+  template <int LPC, int E> __host__ __device__ static size_t lds_need(int D) {
+    return ((size_t)D * LPC * E + (size_t)256 * E) * sizeof(T);
+  }
+  template <int LPC, int E> __host__ __device__ size_t lds_bytes() const {
+    return use_lds ? lds_need<LPC, E>(D) : 0;
+  }
+  template <int LPC, int E> __device__ __forceinline__ GaussLane<T, LPC, E> bind(int) const {
+    GaussLane<T, LPC, E> r;
+    r.mu = mu;
+    r.prec = prec;
+    r.nc = nc;
+    r.D = D;
+    r.sprec = nullptr;
+    r.sd = nullptr;
+    if (use_lds) {  // every thread of the block reaches bind() (kernels return after it)
+      constexpr int S = LPC * E;
+      T* sp = (T*)gm_dyn_lds;
+      const int n = D * S;
+      for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const int j = k / S, i = k - j * S;
+        sp[k] = (i < D) ? prec[(long long)j * D + i] : (T)0;
+      }
+      __syncthreads();
+      r.sprec = sp;
+      r.sd = sp + n + (threadIdx.x / LPC) * S;
+    }
+    return r;
+  }
+};
+template <class T, int LPC, int E> struct GaussLane {
+  const T* mu;
+  const T* prec;
+  T nc;
+  int D;
+  const T* sprec;  // LDS [D][S] or null
+  T* sd;           // LDS slot of this lane group's d [S]
+  template <int LPC_, int E_, bool LOGP>
   __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int lane) const {
+    static_assert(LPC_ == LPC && E_ == E, "layout mismatch");
     T d[E], w[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
       d[e] = (i < D) ? x[e] - mu[i] : (T)0;
     }
-    for (int j = 0; j < D; ++j) {
-      T dj;
-      // coordinate j lives in lane j/E, slot j%E of this chain's group
-      const int src = j / E, slot = j % E;
-      T mine = d[0];
+    if (sprec) {
+      constexpr int S = LPC * E;
+      // the previous evaluation's broadcast reads are done before d is replaced
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int e = 1; e < E; ++e) mine = (slot == e) ? d[e] : mine;
-      if constexpr (LPC == 1) dj = mine;
-      else dj = __shfl(mine, src, LPC);
+      for (int e = 0; e < E; ++e) sd[lane * E + e] = d[e];
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const T* pr = sprec + lane * E;
+      {
+        const T d0 = sd[0];
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int i = lane * E + e;
-        const T pij = (i < D) ? prec[(long long)i * D + j] : (T)0;
-        w[e] = (j == 0) ? pij * dj : w[e] + pij * dj;
+        for (int e = 0; e < E; ++e) w[e] = pr[e] * d0;
+      }
+#pragma unroll 4
+      for (int j = 1; j < D; ++j) {
+        const T dj = sd[j];
+#pragma unroll
+        for (int e = 0; e < E; ++e) w[e] = w[e] + pr[j * S + e] * dj;
+      }
+    } else {
+      // Columns in batches of GU: the batch's global loads and lane
+      // broadcasts are issued together; the accumulation stays in ascending j.
+      constexpr int GU = 8;
+      for (int j0 = 0; j0 < D; j0 += GU) {
+        T pj[GU][E], dj[GU];
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+          const int j = (j0 + u < D) ? j0 + u : D - 1;
+          // coordinate j lives in lane j/E, slot j%E of this chain's group
+          const int src = j / E, slot = j % E;
+          T mine = d[0];
+#pragma unroll
+          for (int e = 1; e < E; ++e) mine = (slot == e) ? d[e] : mine;
+          if constexpr (LPC == 1) dj[u] = mine;
+          else dj[u] = __shfl(mine, src, LPC);
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const int i = lane * E + e;
+            pj[u][e] = (i < D) ? prec[(long long)j * D + i] : (T)0;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < GU; ++u) {
+          if (j0 + u < D) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) w[e] = (j0 + u == 0) ? pj[u][e] * dj[u] : w[e] + pj[u][e] * dj[u];
+          }
+        }
       }
     }
     T part = (T)0;

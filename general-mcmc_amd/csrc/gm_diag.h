@@ -13,12 +13,12 @@ struct DiagScratch {
     if (part) (void)hipFree(part);
   }
 };
-// Per-split-chain means / within variances ([2C][P] each, f64) and the
+// Per-split-chain means / within variances ([P][2C] each, f64) and the
 // autocovariance summed over this process's split chains ([h][P], f64).
 int diag_series(gm_dtype dt, const void* x, long long C, long long N, long long P, long long sc,
                 long long sd, long long sp, double* cm, double* s2, double* acov_sum,
                 DiagScratch& ws, hipStream_t st);
-// From K split chains' cm/s2 ([K][P]) and R ranks' acov sums ([R][h][P]).
+// From R ranks' cm/s2 ([R][P][K/R], K split chains in all) and acov sums ([R][h][P]).
 int diag_final(const double* cm, const double* s2, const double* acov, long long K, int R, int h,
                long long P, float* rhat_dev, float* ess_dev, hipStream_t st);
 }  // namespace gm

@@ -18,7 +18,7 @@ struct TargetDev {
   int D = 0;
   double a = 1, b = 100, std = 1, norm_const = 0;
   const void* mu = nullptr;    // [D] of the sampler dtype
-  const void* prec = nullptr;  // [D*D] of the sampler dtype
+  const void* prec = nullptr;  // [D*D] of the sampler dtype, transposed (prec[j*D+i] = P_ij)
 };
 
 struct Layout {

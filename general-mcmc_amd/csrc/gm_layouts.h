@@ -52,6 +52,8 @@ hipError_t dispatch_target(const TargetDev& tg, F& f) {
       t.prec = (const T*)tg.prec;
       t.nc = (T)tg.norm_const;
       t.D = tg.D;
+      // LDS staging while it leaves room for >= 4 blocks (16 waves) per CU
+      t.use_lds = GaussT<T>::template lds_need<LPC, E>(tg.D) <= 40 * 1024;
       return f.template operator()<T, LPC, E>(t);
     }
     default:

@@ -100,7 +100,8 @@ hipError_t launch_mh(gm_dtype dt, const TargetDev& tg, const Layout& lay, const 
   return dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
     const long long threads = a.C * LPC;
     const unsigned blocks = (unsigned)((threads + 255) / 256);
-    hipLaunchKernelGGL((mh_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), 0, st, a, t);
+    const size_t lds = t.template lds_bytes<LPC, E>();
+    hipLaunchKernelGGL((mh_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), lds, st, a, t);
     return hipGetLastError();
   });
 }

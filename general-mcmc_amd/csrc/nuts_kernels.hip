@@ -1004,7 +1004,8 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     hipError_t e = dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
       const long long threads = C * LPC;
       const unsigned blocks = (unsigned)((threads + 255) / 256);
-      hipLaunchKernelGGL((nuts_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), 0, st, a, t);
+      const size_t lds = t.template lds_bytes<LPC, E>();
+      hipLaunchKernelGGL((nuts_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), lds, st, a, t);
       return hipGetLastError();
     });
     if (e != hipSuccess) {

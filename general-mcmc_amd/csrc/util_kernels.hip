@@ -37,7 +37,8 @@ hipError_t launch_logp_grad(gm_dtype dt, const TargetDev& tg, const Layout& lay,
   return dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
     const long long threads = n * LPC;
     const unsigned blocks = (unsigned)((threads + 255) / 256);
-    hipLaunchKernelGGL((logp_grad_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), 0, st, n,
+    const size_t lds = t.template lds_bytes<LPC, E>();
+    hipLaunchKernelGGL((logp_grad_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), lds, st, n,
                        tg.D, (const T*)x, (T*)logp, (T*)grad, t);
     return hipGetLastError();
   });

@@ -142,7 +142,10 @@ def test_nuts_chain_1_kat(gm):
     np.testing.assert_array_equal(c.run(1, 0), [[0.0, 1.0]])
 
 
-@pytest.mark.parametrize("shape", [(4, 100, 3), (7, 41, 2), (64, 300, 5), (3, 1000, 1)])
+# h = N/2 <= 64 runs the matrix-core Gram kernel (chain groups, 8-parameter
+# tiles: C and P chosen off those multiples), larger h the direct-lag kernel
+@pytest.mark.parametrize("shape", [(4, 100, 3), (7, 41, 2), (64, 300, 5), (3, 1000, 1),
+                                   (100, 128, 37), (33, 129, 17), (517, 60, 9), (9, 131, 3)])
 @pytest.mark.parametrize("dtype", DTYPES)
 def test_split_rhat_ess_matches_oracle(gm, oracle, shape, dtype):
     rng = np.random.default_rng(sum(shape))
