@@ -111,6 +111,32 @@ template <int LPC, class T> __device__ __forceinline__ T from_prev(T v) {
   else return dpp<DPP_WAVE_SHR1>(v);
 }
 
+// A chain spread over the W waves of one workgroup (hmc_wide_kernel, for
+// dim > 1024): thread t of the block holds coordinates [t*E, (t+1)*E). Per-
+// chain sums are each wave's 64-lane total (the group_sum<64> order) added
+// over the waves left to right; Rosenbrock's neighbour values cross wave
+// boundaries through LDS (double-buffered, one barrier per evaluation).
+constexpr int GM_WIDE_MAX_WAVES = 16;
+// threads per chain the wide kernels allow for E elements of esz bytes: up
+// to 32 bytes per lane in 1024 threads (128 VGPRs), more in 512 (256 VGPRs)
+__host__ __device__ constexpr int gm_wide_max_threads(int esz, int E) { return esz * E <= 32 ? 1024 : 512; }
+template <class T> struct WideCtx {
+  int w, W, lane;  // wave in the block, waves per chain, lane in the wave
+  T* xfirst;       // LDS [2][16]: x[0] of each wave's lane 0
+  T* xxlast;       // LDS [2][16]: x[E-1]^2 of each wave's lane 63
+  T* red;          // LDS [16]: wave totals
+  int par;         // buffer parity of the next evaluation
+};
+template <class T> __device__ __forceinline__ T block_sum(T v, const WideCtx<T>& c) {
+  v = group_sum<64>(v);  // wave total, wave-uniform
+  if (c.lane == 0) c.red[c.w] = v;
+  __syncthreads();
+  T s = c.red[0];
+  for (int k = 1; k < c.W; ++k) s = s + c.red[k];
+  __syncthreads();  // red is reused by the next sum
+  return s;
+}
+
 // Branch-free "c ? v : +0" with a per-lane mask the compiler cannot see
 // through (an empty asm), so it stays one v_and per use instead of being
 // turned back into a select and then into a divergent branch around the
@@ -145,7 +171,7 @@ template <class T> struct RosenbrockT {
   template <int LPC, int E> __host__ __device__ size_t lds_bytes() const { return 0; }
   template <int LPC, int E> __device__ __forceinline__ RosenbrockLane<T, E> bind(int lane) const {
     RosenbrockLane<T, E> r;
-    r.a = a; r.b = b; r.b2 = b2; r.b4 = b4;
+    r.a = a; r.b = b; r.b2 = b2; r.b4 = b4; r.Dc = D;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
@@ -160,6 +186,7 @@ template <class T> struct RosenbrockT {
 };
 template <class T, int E> struct RosenbrockLane {
   T a, b, b2, b4;
+  int Dc;
   typename MaskOf<T>::type ms[E], mp[E];  // [i <= D-2], [1 <= i <= D-1]
   T b4m[E], c2m[E], b2m[E];               // 4b, 2, 2b where those masks hold, else 0
   template <int LPC, int E_, bool LOGP>
@@ -228,6 +255,73 @@ template <class T, int E> struct RosenbrockLane {
     if (LOGP) return -group_sum<LPC>(part);
     return (T)0;
   }
+  // The 64-lane form above for a chain spread over a workgroup: the wave-
+  // boundary neighbours come from LDS instead of reading 0 (same operands,
+  // same bits as a single group holding the whole chain). The [.] factors
+  // are the constants themselves in waves without a chain-end coordinate
+  // (wave-uniform branch) and are derived from the index in the two others,
+  // instead of 5*E per-lane registers.
+  template <int E_, bool LOGP>
+  __device__ __forceinline__ T eval_wide(const T (&x)[E], T (&g)[E], WideCtx<T>& c) const {
+    static_assert(E_ == E, "layout mismatch");
+    const int bb = c.par * GM_WIDE_MAX_WAVES;
+    c.par ^= 1;
+    const T xxl = x[E - 1] * x[E - 1];
+    if (c.lane == 0) c.xfirst[bb + c.w] = x[0];
+    if (c.lane == 63) c.xxlast[bb + c.w] = xxl;
+    __syncthreads();
+    const T bnx = (c.w + 1 < c.W) ? c.xfirst[bb + c.w + 1] : (T)0;  // wave-uniform reads
+    const T bpxx = (c.w > 0) ? c.xxlast[bb + c.w - 1] : (T)0;
+    T nx = from_next<64>(x[0]);
+    T pxx = from_prev<64>(xxl);
+    nx = (c.lane == 63) ? bnx : nx;
+    pxx = (c.lane == 0) ? bpxx : pxx;
+    const int D = Dc;
+    const int i0 = (c.w * 64 + c.lane) * E;
+    const bool interior = c.w * 64 * E >= 1 && (c.w * 64 + 63) * E + E - 1 <= D - 2;
+    T part = (T)0;
+    // streamed over e (t_e computed when first needed, carried as t_{e-1})
+    T tprev = x[0] - pxx;
+    if (interior) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const T xn = (e + 1 < E) ? x[(e + 1 < E) ? e + 1 : e] : nx;
+        const T te = xn - x[e] * x[e];
+        const T am = a - x[e];
+        const T A = (b4 * x[e]) * te + (T)2 * am;
+        const T B = b2 * tprev;
+        g[e] = A - B;
+        if (LOGP) {
+          const T s = b * (te * te) + am * am;
+          part = (e == 0) ? s : part + s;
+        }
+        tprev = te;
+      }
+    } else {
+      // an opaque copy of D keeps the per-element factors from being hoisted
+      // out of the leapfrog loop into 3*E loop-invariant registers
+      int Dv = D;
+      asm volatile("" : "+s"(Dv));
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = i0 + e;
+        const bool hs = i <= Dv - 2, hp = (i >= 1) & (i <= Dv - 1);
+        const T xn = (e + 1 < E) ? x[(e + 1 < E) ? e + 1 : e] : nx;
+        const T te = xn - x[e] * x[e];
+        const T am = a - x[e];
+        const T A = ((hs ? b4 : (T)0) * x[e]) * te + (hs ? (T)2 : (T)0) * am;
+        const T B = (hp ? b2 : (T)0) * tprev;
+        g[e] = A - B;
+        if (LOGP) {
+          const T s = hs ? b * (te * te) + am * am : (T)0;
+          part = (e == 0) ? s : part + s;
+        }
+        tprev = te;
+      }
+    }
+    if (LOGP) return -block_sum(part, c);
+    return (T)0;
+  }
 };
 
 // IsotropicGaussian as a target (distributions.rs:398-406):
@@ -250,6 +344,22 @@ template <class T> struct IsoGaussT {
       }
     }
     if (LOGP) return ((T)-0.5 * group_sum<LPC>(part)) / var;
+    return (T)0;
+  }
+  template <int E, bool LOGP>
+  __device__ __forceinline__ T eval_wide(const T (&x)[E], T (&g)[E], WideCtx<T>& c) const {
+    const int t0 = (c.w * 64 + c.lane) * E;
+    T part = (T)0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = t0 + e;
+      g[e] = (i < D) ? (-x[e]) / var : (T)0;
+      if (LOGP) {
+        const T s = (i < D) ? x[e] * x[e] : (T)0;
+        part = (e == 0) ? s : part + s;
+      }
+    }
+    if (LOGP) return ((T)-0.5 * block_sum(part, c)) / var;
     return (T)0;
   }
 };

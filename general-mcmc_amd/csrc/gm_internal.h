@@ -26,6 +26,11 @@ struct Layout {
   int elems = 1;
 };
 bool layout_supported(int lanes, int elems);
+// one chain per workgroup of lanes/64 waves (HMC only, dim > 1024)
+inline bool layout_is_wide(const Layout& l) { return l.lanes > 64; }
+bool wide_layout_supported(int lanes, int elems, gm_dtype dt);
+// largest dim of the wide path (f32; f64 is half of it)
+constexpr int GM_WIDE_MAX_DIM = 16384;
 Layout default_layout(int D, gm_dtype dt, int kind);
 
 // ---- HMC -------------------------------------------------------------------
@@ -46,6 +51,7 @@ struct HmcLaunch {
   long long sample_row0 = 0;    // ... at row sample_row0 + (s - collect_from)
   int lf_unroll = 1;            // leapfrog loop unroll (1 or 4; same results)
   int stagger = 1;              // per-wave staggered prefetch of the draw blocks (same results)
+  void* zs = nullptr;           // wide layouts: momentum block scratch [C][S][lanes*elems]
 };
 hipError_t launch_hmc(gm_dtype dt, const TargetDev& tg, const Layout& lay, const HmcLaunch& a,
                       hipStream_t st);

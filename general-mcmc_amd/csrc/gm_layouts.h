@@ -75,4 +75,46 @@ hipError_t dispatch(gm_dtype dt, const TargetDev& tg, const Layout& lay, F&& f) 
   return hipErrorInvalidValue;
 }
 
+// Wide layouts (one chain per workgroup of lanes/64 waves; HMC, dim > 1024):
+// elems in {4, 8, 16, 32} (f64: 4, 8, 16), lanes up to gm_wide_max_threads,
+// the targets with a wide evaluation (Rosenbrock, isotropic Gaussian). Calls
+// f.template operator()<T, E>(target).
+#define GM_WIDE_ELEMS_LIST(X) X(4) X(8) X(16) X(32)
+template <class T, int E, class F>
+hipError_t dispatch_wide_target(const TargetDev& tg, F& f) {
+  switch (tg.kind) {
+    case GM_TARGET_ROSENBROCK: {
+      RosenbrockT<T> t;
+      t.a = (T)tg.a;
+      t.b = (T)tg.b;
+      t.b2 = (T)2 * (T)tg.b;
+      t.b4 = (T)4 * (T)tg.b;
+      t.D = tg.D;
+      return f.template operator()<T, E>(t);
+    }
+    case GM_TARGET_ISO_GAUSS: {
+      IsoGaussT<T> t;
+      t.var = (T)tg.std * (T)tg.std;
+      t.D = tg.D;
+      return f.template operator()<T, E>(t);
+    }
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+template <class F>
+hipError_t dispatch_wide(gm_dtype dt, const TargetDev& tg, const Layout& lay, F&& f) {
+  if (lay.lanes % 64 || lay.lanes > gm_wide_max_threads(dt == GM_F32 ? 4 : 8, lay.elems))
+    return hipErrorInvalidValue;
+#define GM_TRY_WIDE(E_)                                                                     \
+  if (lay.elems == E_) {                                                                    \
+    if (dt == GM_F32) return dispatch_wide_target<float, E_>(tg, f);                        \
+    if constexpr (E_ <= 16) return dispatch_wide_target<double, E_>(tg, f);                 \
+    return hipErrorInvalidValue;                                                            \
+  }
+  GM_WIDE_ELEMS_LIST(GM_TRY_WIDE)
+#undef GM_TRY_WIDE
+  return hipErrorInvalidValue;
+}
+
 }  // namespace gm

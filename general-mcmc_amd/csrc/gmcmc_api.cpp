@@ -34,6 +34,12 @@ bool layout_supported(int lanes, int elems) {
   return false;
 }
 
+bool wide_layout_supported(int lanes, int elems, gm_dtype dt) {
+  const int esz = dt == GM_F32 ? 4 : 8;
+  if (!(elems == 4 || elems == 8 || elems == 16 || (elems == 32 && dt == GM_F32))) return false;
+  return lanes > 64 && lanes % 64 == 0 && lanes <= gm_wide_max_threads(esz, elems);
+}
+
 static int next_pow2(int v) {
   int p = 1;
   while (p < v) p <<= 1;
@@ -44,6 +50,26 @@ Layout default_layout(int D, gm_dtype dt, int kind) {
   (void)dt;
   (void)kind;
   Layout l;
+  if (D > 1024) {
+    // wide: the smallest elems whose workgroup holds the chain, so that a
+    // chain gets as many waves as possible (few huge chains fill more of the
+    // GPU): f32 4 / 8 (1024 threads), 32 (512); f64 4 (1024), 16 (512)
+    const int esz = dt == GM_F32 ? 4 : 8;
+    const int cand[4] = {4, 8, 16, 32};
+    for (int k = 0; k < 4; ++k) {
+      const int E = cand[k];
+      if (!wide_layout_supported(128, E, dt)) continue;
+      const int W = (D + 64 * E - 1) / (64 * E);
+      if (W * 64 <= gm_wide_max_threads(esz, E)) {
+        l.elems = E;
+        l.lanes = 64 * (W < 2 ? 2 : W);
+        return l;
+      }
+    }
+    l.elems = 32;
+    l.lanes = 512;  // beyond the supported dims (build_target rejects them)
+    return l;
+  }
   if (D <= 64) {
     l.elems = 1;
     l.lanes = next_pow2(D < 1 ? 1 : D);
@@ -111,6 +137,8 @@ struct gm_sampler {
   size_t samples_bytes = 0;
   void* d_tmp = nullptr;
   size_t tmp_bytes = 0;
+  void* d_zs = nullptr;  // wide-layout HMC momentum scratch
+  size_t zs_bytes = 0;
   Layout lay;
   long long steps_per_launch = 1000;
   std::vector<hipEvent_t> evs;
@@ -192,7 +220,10 @@ int gm::build_target(const gm_target* t, gm_dtype dt, long long dim, TargetDev* 
                      void** d_prec) {
   GM_REQ(t != nullptr, "target is NULL");
   GM_REQ(t->dim == dim, "target dim does not match the sampler dim");
-  GM_REQ(dim >= 1 && dim <= 1024, "dim must be in [1, 1024]");
+  GM_REQ(dim >= 1 && dim <= (dt == GM_F32 ? GM_WIDE_MAX_DIM : GM_WIDE_MAX_DIM / 2),
+         "dim must be in [1, 16384] (f32) / [1, 8192] (f64)");
+  GM_REQ(dim <= 1024 || t->kind == GM_TARGET_ROSENBROCK || t->kind == GM_TARGET_ISO_GAUSS,
+         "dim > 1024 is supported for the Rosenbrock and isotropic Gaussian targets");
   out->kind = t->kind;
   out->D = (int)dim;
   out->a = t->a;
@@ -366,6 +397,7 @@ static int create_common(int kind, const gm_target* target, gm_dtype dtype, int6
   GM_REQ(init != nullptr, "init is NULL");
   GM_REQ(chain_offset >= 0 && chain_offset + n_chains <= 0xffffffffLL,
          "global chain ids must fit in 32 bits");
+  GM_REQ(dim <= 1024 || kind == K_HMC, "dim > 1024 is supported by the HMC sampler only");
   gm_sampler* s = new gm_sampler();
   s->kind = kind;
   s->dt = dtype;
@@ -460,7 +492,10 @@ int gm_sampler_layout(gm_sampler* s, int32_t* lanes, int32_t* elems) {
 
 int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems) {
   GM_REQ(s, "sampler is NULL");
-  GM_REQ(layout_supported(lanes, elems), "layout (lanes, elems) is not compiled in");
+  const bool wide = lanes > 64;
+  GM_REQ(wide ? wide_layout_supported(lanes, elems, s->dt) : layout_supported(lanes, elems),
+         "layout (lanes, elems) is not compiled in");
+  GM_REQ(!wide || s->kind == K_HMC, "wide layouts (lanes > 64) are for the HMC sampler");
   GM_REQ((long long)lanes * elems >= s->D, "lanes*elems must cover dim");
   GM_REQ((long long)lanes * elems < 2LL * s->D || lanes == 1 ||
              ((long long)(lanes / 2) * elems < s->D),
@@ -556,6 +591,12 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
       {
         const char* v = getenv("GM_HMC_STAGGER");  // measurement knob
         a.stagger = v ? (atoi(v) != 0) : 1;
+      }
+      if (layout_is_wide(s->lay)) {
+        const size_t need = (size_t)s->C * (s->dt == GM_F32 ? 4 : 2) * s->lay.lanes * s->lay.elems * s->esz;
+        int rc = ensure_buf(&s->d_zs, &s->zs_bytes, need);
+        if (rc) return rc;
+        a.zs = s->d_zs;
       }
       e = launch_hmc(s->dt, s->tg, s->lay, a, s->stream);
     } else {
@@ -965,6 +1006,7 @@ int gm_destroy(gm_sampler* s) {
   for (auto ev : s->evs) hipEventDestroy(ev);
   if (s->d_mu) hipFree(s->d_mu);
   if (s->d_prec) hipFree(s->d_prec);
+  if (s->d_zs) hipFree(s->d_zs);
   if (s->d_q) hipFree(s->d_q);
   if (s->d_logp) hipFree(s->d_logp);
   if (s->d_acc) hipFree(s->d_acc);

@@ -207,8 +207,132 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// hmc_wide_kernel: the same transition for dim > 1024, one chain per
+// workgroup of W = blockDim/64 waves (WideCtx in gm_device.h). The per-step
+// momenta of a draw block (S transitions) go to a per-chain scratch in HBM
+// (each thread re-reads only what it wrote), the accept log-uniforms stay in
+// registers; every per-chain sum is a block reduction, so the accept branch is
+// uniform over the workgroup. The reference's 10,000-dimensional Rosenbrock
+// benchmark (hmc.rs:757-791) runs here.
+template <class T, int E, class TG>
+__global__ __launch_bounds__(gm_wide_max_threads(sizeof(T), E)) void hmc_wide_kernel(HmcLaunch a, TG tg_) {
+  __shared__ T xf[2 * GM_WIDE_MAX_WAVES], xl[2 * GM_WIDE_MAX_WAVES], red[GM_WIDE_MAX_WAVES];
+  const int tid = threadIdx.x;
+  const long long c = blockIdx.x;
+  const auto tg = tg_.template bind<64, E>(tid);  // coordinates tid*E + e
+  WideCtx<T> cx{tid >> 6, (int)(blockDim.x >> 6), tid & 63, xf, xl, red, 0};
+  const int D = a.D;
+  const long long Dp = (long long)blockDim.x * E;
+  T* __restrict__ qs = (T*)a.q;
+  const T eps = (T)a.eps;
+  const T half = (T)0.5 * eps;
+  const uint32_t cid = a.chain_offset + (uint32_t)c;
+  constexpr int S = Blk<T>::S;
+  T* __restrict__ zs = (T*)a.zs + c * S * Dp;
+  // q: current position; g1: the gradient at q1, which is the current
+  // position at every transition start (a rejected proposal re-evaluates the
+  // gradient at q instead of keeping a copy: same bits, E fewer registers)
+  T q[E], q1[E], p1[E], g1[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = tid * E + e;
+    q[e] = (i < D) ? qs[c * D + i] : (T)0;
+  }
+  T lp = tg.template eval_wide<E, true>(q, g1, cx);
+#pragma unroll
+  for (int e = 0; e < E; ++e) q1[e] = q[e];
+  long long acc = 0;
+  T lus[S];
+  for (int s = 0; s < a.n_steps; ++s) {
+    const uint64_t st = a.step0 + (uint64_t)s;
+    const int k0 = (int)(st % S);
+    if (s == 0 || k0 == 0) {  // draw block st/S: momenta to scratch, accept logs to registers
+#pragma unroll 1
+      for (int e = 0; e < E; ++e) {
+        const int i = tid * E + e;
+        T z[S];
+        normals_of(draw_block(a.seed, cid, st / S, TAG_MOM, (uint32_t)i), z);
+#pragma unroll
+        for (int k = 0; k < S; ++k) zs[k * Dp + i] = (i < D) ? z[k] : (T)0;
+      }
+      T us[S];
+      uniforms_of(draw_block(a.seed, cid, st / S, TAG_ACC, 0u), us);
+#pragma unroll
+      for (int k = 0; k < S; ++k) lus[k] = glog_unif(us[k]);
+    }
+    // 1-2. momentum ~ N(0, I) and its kinetic energy
+    T kp = (T)0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      p1[e] = zs[k0 * Dp + tid * E + e];
+      const T sq = p1[e] * p1[e];
+      kp = (e == 0) ? sq : kp + sq;
+    }
+    const T ke0 = block_sum(kp, cx) * (T)0.5;
+    T lnu = lus[0];
+#pragma unroll
+    for (int k = 1; k < S; ++k) lnu = (k0 == k) ? lus[k] : lnu;
+    // 4-5. proposal and leapfrog (q1 = q and g1 = grad(q) here)
+    T lp1 = lp;
+    for (int l = 0; l < a.L; ++l) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+#pragma unroll
+      for (int e = 0; e < E; ++e) q1[e] = q1[e] + p1[e] * eps;
+      if (l + 1 < a.L) tg.template eval_wide<E, false>(q1, g1, cx);
+      else lp1 = tg.template eval_wide<E, true>(q1, g1, cx);
+#pragma unroll
+      for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+    }
+    // 6. proposed kinetic energy
+    T kq = (T)0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const T sq = p1[e] * p1[e];
+      kq = (e == 0) ? sq : kq + sq;
+    }
+    const T ke1 = block_sum(kq, cx) * (T)0.5;
+    // 7-9. Metropolis accept (NaN log_alpha rejects); block-uniform
+    const T log_alpha = (lp1 - lp) + (ke0 - ke1);
+    if (log_alpha >= lnu) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) q[e] = q1[e];
+      lp = lp1;
+      ++acc;
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) q1[e] = q[e];
+      if (a.L > 0) tg.template eval_wide<E, false>(q1, g1, cx);
+    }
+    if (s >= a.collect_from) {
+      T* __restrict__ out = (T*)a.samples + ((a.sample_row0 + (s - a.collect_from)) * a.C + c) * D;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = tid * E + e;
+        if (i < D) out[i] = q[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = tid * E + e;
+    if (i < D) qs[c * D + i] = q[e];
+  }
+  if (tid == 0) {
+    ((T*)a.logp)[c] = lp;
+    a.accepts[c] += acc;
+  }
+}
+
 hipError_t launch_hmc(gm_dtype dt, const TargetDev& tg, const Layout& lay, const HmcLaunch& a,
                       hipStream_t st) {
+  if (layout_is_wide(lay)) {
+    return dispatch_wide(dt, tg, lay, [&]<class T, int E, class TG>(TG t) -> hipError_t {
+      hipLaunchKernelGGL((hmc_wide_kernel<T, E, TG>), dim3((unsigned)a.C), dim3(lay.lanes), 0, st, a, t);
+      return hipGetLastError();
+    });
+  }
   return dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
     const long long threads = a.C * LPC;
     const unsigned blocks = (unsigned)((threads + 255) / 256);

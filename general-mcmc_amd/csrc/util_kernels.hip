@@ -32,8 +32,43 @@ __global__ __launch_bounds__(256) void logp_grad_kernel(long long n, int D, cons
   if (lane == 0 && logp) logp[c] = lp;
 }
 
+// dim > 1024: one point per workgroup (the wide layout of hmc_wide_kernel)
+template <class T, int E, class TG>
+__global__ __launch_bounds__(gm_wide_max_threads(sizeof(T), E)) void logp_grad_wide_kernel(int D, const T* __restrict__ x,
+                                                             T* __restrict__ logp,
+                                                             T* __restrict__ grad, TG tg_) {
+  __shared__ T xf[2 * GM_WIDE_MAX_WAVES], xl[2 * GM_WIDE_MAX_WAVES], red[GM_WIDE_MAX_WAVES];
+  const int tid = threadIdx.x;
+  const long long c = blockIdx.x;
+  const auto tg = tg_.template bind<64, E>(tid);
+  WideCtx<T> cx{tid >> 6, (int)(blockDim.x >> 6), tid & 63, xf, xl, red, 0};
+  T q[E], g[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = tid * E + e;
+    q[e] = (i < D) ? x[c * D + i] : (T)0;
+  }
+  const T lp = tg.template eval_wide<E, true>(q, g, cx);
+  if (grad) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = tid * E + e;
+      if (i < D) grad[c * D + i] = g[e];
+    }
+  }
+  if (tid == 0 && logp) logp[c] = lp;
+}
+
 hipError_t launch_logp_grad(gm_dtype dt, const TargetDev& tg, const Layout& lay, long long n,
                             const void* x, void* logp, void* grad, hipStream_t st) {
+  if (layout_is_wide(lay)) {
+    if (n == 0) return hipSuccess;
+    return dispatch_wide(dt, tg, lay, [&]<class T, int E, class TG>(TG t) -> hipError_t {
+      hipLaunchKernelGGL((logp_grad_wide_kernel<T, E, TG>), dim3((unsigned)n), dim3(lay.lanes), 0, st,
+                         tg.D, (const T*)x, (T*)logp, (T*)grad, t);
+      return hipGetLastError();
+    });
+  }
   return dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
     const long long threads = n * LPC;
     const unsigned blocks = (unsigned)((threads + 255) / 256);

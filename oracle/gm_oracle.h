@@ -19,7 +19,8 @@
  * Summation order: per-chain sums (kinetic energy, log-density, U-turn dots)
  * are taken in the engine's declared order, parameterised by the lane layout
  * (lanes x elems): each lane sums its elems left to right, then an xor
- * butterfly over lanes (offsets 1, 2, 4, ...).
+ * butterfly over lanes (offsets 1, 2, 4, ...). Layouts wider than one wave
+ * (lanes = 64*W, HMC for dim > 1024) add the W wave totals left to right.
  */
 #ifndef GM_ORACLE_H
 #define GM_ORACLE_H
@@ -28,6 +29,9 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+/* largest dimension of the wide (one chain per workgroup) HMC path */
+#define GM_MAX_DIM 16384
 
 typedef struct or_target {
   int32_t kind; /* 1 rosenbrock, 2 iso gauss, 3 gauss */

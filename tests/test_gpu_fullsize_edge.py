@@ -150,7 +150,7 @@ def test_bad_arguments_raise(gm):
         s.set_layout(2, 1)  # does not cover dim
     with pytest.raises(gm.GMError):
         s.set_layout(3, 1)  # not compiled
-    with pytest.raises(gm.GMError):
-        gm.HMC(gm.RosenbrockND(), gm.init_det(2, 1025), 0.1, 2)
+    with pytest.raises(gm.GMError):  # beyond the wide path (f32 16384, f64 8192)
+        gm.HMC(gm.RosenbrockND(), gm.init_det(2, 16385, np.float32), 0.1, 2)
     with pytest.raises(gm.GMError):
         gm.split_rhat_mean_ess(np.zeros((2, 1, 3)))
