@@ -7,6 +7,7 @@ config size, with ESS from the device diagnostics.
   cfg4  HMC RosenbrockND 128-D f32, 65536 chains / 8 GPUs = 8192 per GPU
   cfg5  MH IsotropicGaussian(1) 256-D f64, proposal sd 2.38/sqrt(256),
         131072 chains / 8 GPUs = 16384 per GPU
+  10k   the reference's test_bench_10000d (6 chains x 10,000-D, wide layout)
 """
 import argparse
 import json
@@ -82,8 +83,23 @@ def cfg5(a):
             "ess_mean": float(ess.mean()), "ess_per_s": float(ess.mean()) / t}
 
 
+def ref10k(a):
+    """test_bench_10000d (hmc.rs:757-791): 6 chains x 10,000-D RosenbrockND
+    f32, eps 0.01, L 50, run(100, 100) -- the reference's own HMC benchmark."""
+    dim, n = 10000, 6
+    x0 = np.repeat(gm.init_with_seed(1, dim, 42, np.float32), n, axis=0)
+    s = gm.HMC(gm.RosenbrockND(), x0, 0.01, 50).set_seed(42)
+    s.run_positions(1, 0)  # warm (module load)
+    s = gm.HMC(gm.RosenbrockND(), x0, 0.01, 50).set_seed(42)
+    out, t = timed(lambda: s.run(100, 100))
+    assert out.shape == (n, 100, dim)
+    return {"config": "ref test_bench_10000d HMC Rosenbrock10000 f32 6 chains run(100,100)",
+            "chains": n, "layout": "%dx%d" % s.layout(), "wall_s": t,
+            "chain_leapfrog_per_s": n * 200 * 50 / t, "includes": "D2H of the [6,100,10000] sample"}
+
+
 p = argparse.ArgumentParser()
-p.add_argument("--which", default="3,4,5")
+p.add_argument("--which", default="3,4,5,10k")
 p.add_argument("--nuts-chains", type=int, default=8192)
 p.add_argument("--nuts-discard", type=int, default=500)
 p.add_argument("--nuts-collect", type=int, default=500)
@@ -94,5 +110,5 @@ p.add_argument("--mh-layout", default="")
 a = p.parse_args()
 out = []
 for w in a.which.split(","):
-    r = {"3": cfg3, "4": cfg4, "5": cfg5}[w](a)
+    r = {"3": cfg3, "4": cfg4, "5": cfg5, "10k": ref10k}[w](a)
     print(json.dumps(r), flush=True)
