@@ -365,8 +365,11 @@ template <class T> struct IsoGaussT {
 };
 
 // Dense Gaussian (DiffableGaussian2D generalised, distributions.rs:257-292):
-//   d = x - mu; w_k = sum_j P_kj d_j (j ascending); logp = nc - 0.5*sum_k w_k d_k;
+//   d = x - mu; w_k = sum_j P_kj d_j; logp = nc - 0.5*sum_k w_k d_k;
 //   g = -w   (= -0.5 (P + P^T) d for symmetric P, the autodiff result)
+// The product is an fma chain in ascending j, w = fma(P_kj, d_j, w) from
+// w = 0 (the reference's matmul goes through ndarray/matrixmultiply, whose
+// order and FMA use are its own; the oracle defines this one).
 //
 // The precision matrix is stored transposed (prec[j*D + i] = P_ij) so that
 // lane i's column-j reads are consecutive across the chain's lanes. When it
@@ -376,6 +379,10 @@ template <class T> struct IsoGaussT {
 // LDS slot from which coordinate j is read as a broadcast: per column one LDS
 // read of P and one broadcast read of d_j, no shuffles, no global loads.
 extern __shared__ __attribute__((aligned(16))) unsigned char gm_dyn_lds[];
+
+// fused multiply-add, one rounding (the oracle's FMA)
+__device__ __forceinline__ float gfma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double gfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
 template <class T, int LPC, int E> struct GaussLane;
 template <class T> struct GaussT {
@@ -444,13 +451,13 @@ template <class T, int LPC, int E> struct GaussLane {
       {
         const T d0 = sd[0];
 #pragma unroll
-        for (int e = 0; e < E; ++e) w[e] = pr[e] * d0;
+        for (int e = 0; e < E; ++e) w[e] = gfma(pr[e], d0, (T)0);
       }
 #pragma unroll 4
       for (int j = 1; j < D; ++j) {
         const T dj = sd[j];
 #pragma unroll
-        for (int e = 0; e < E; ++e) w[e] = w[e] + pr[j * S + e] * dj;
+        for (int e = 0; e < E; ++e) w[e] = gfma(pr[j * S + e], dj, w[e]);
       }
     } else {
       // Columns in batches of GU: the batch's global loads and lane
@@ -478,7 +485,7 @@ template <class T, int LPC, int E> struct GaussLane {
         for (int u = 0; u < GU; ++u) {
           if (j0 + u < D) {
 #pragma unroll
-            for (int e = 0; e < E; ++e) w[e] = (j0 + u == 0) ? pj[u][e] * dj[u] : w[e] + pj[u][e] * dj[u];
+            for (int e = 0; e < E; ++e) w[e] = gfma(pj[u][e], dj[u], (j0 + u == 0) ? (T)0 : w[e]);
           }
         }
       }

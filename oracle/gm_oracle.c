@@ -302,6 +302,7 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #define LOG or_log_d
 #define EXP or_exp_d
 #define SQRT sqrt
+#define FMA fma
 #define NORMAL or_normal_d
 #define UNIF_CO or_uniform_co_d
 #define UNIF_OC uniform_oc_d
@@ -312,6 +313,7 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #undef LOG
 #undef EXP
 #undef SQRT
+#undef FMA
 #undef NORMAL
 #undef UNIF_CO
 #undef UNIF_OC
@@ -322,6 +324,7 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #define LOG or_log_f
 #define EXP or_exp_f
 #define SQRT sqrtf
+#define FMA fmaf
 #define NORMAL or_normal_f
 #define UNIF_CO or_uniform_co_f
 #define UNIF_OC uniform_oc_f
