@@ -125,7 +125,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "leapfrog steps/sec (whole node) + ESS/sec, 64-dim Rosenbrock HMC",
+            "metric": "leapfrog steps/sec (whole node) + ESS/sec, 64-dim Rosenbrock HMC at 1/2/4/8 GPUs",
             "value": value,
             "unit": "chain-leapfrog steps/s",
             "n_gpus": world,
