@@ -106,16 +106,24 @@ def main():
     flops_lf = 15 * (D - 1) + 6 * D  # RosenbrockND logp+grad and kick/drift/kick per chain-leapfrog
     achieved_tflops = flops_lf * C_loc * L * steps_per_launch / (launch_ms * 1e-3) / 1e12
 
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
+    # PMC-derived figures of this exact launch shape (profiles/, from the
+    # rocprofv3 passes of tools/profile_bench.sh and tools/pmc_sq.sh)
+    key = f"C{C_loc}_D{D}_L{L}_K{a.steps}_{a.dtype}"
+
+    def pmc(name):
+        path = os.path.join(ROOT, "profiles", name)
         try:
-            pm = json.load(open(pmc_path))
-            key = f"C{C_loc}_D{D}_L{L}_K{a.steps}_{a.dtype}"
-            if key in pm:
-                traffic = pm[key]["hbm_bytes_per_launch"]
+            return json.load(open(path)).get(key) if os.path.exists(path) else None
         except Exception:
-            traffic = None
+            return None
+
+    tr = pmc("pmc_traffic.json")
+    traffic = tr["hbm_bytes_per_launch"] if tr else None
+    vi = pmc("pmc_valu.json")
+    valu_issue = None if not vi else {
+        "frac": vi["issue_frac"], "frac_at_2p4ghz": vi["issue_frac_at_2p4ghz"],
+        "valu_insts_per_wave": vi["valu_insts_per_wave"], "clock_ghz": vi["clock_ghz"],
+        "note": "SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) / (1024 SIMDs x kernel cycles)"}
 
     copy_gbs = copy_ceiling(lib) if rank == 0 else None
 
@@ -152,7 +160,8 @@ def main():
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "valu": {"achieved_tflops": achieved_tflops,
                                   "peak_tflops": VALU_F32_PEAK_TFLOPS,
-                                  "frac": achieved_tflops / VALU_F32_PEAK_TFLOPS},
+                                  "frac": achieved_tflops / VALU_F32_PEAK_TFLOPS,
+                                  "issue": valu_issue},
                          "copy_ceiling_gbs": copy_gbs},
             "cpu_baseline": cpu,
         }
