@@ -81,8 +81,12 @@ def main():
     barrier_sync()
     t0 = time.perf_counter()
     ds = sampler.run_positions(a.steps, 0)
-    barrier_sync()
+    # each rank's clock stops at its own device synchronize; the closing
+    # barrier follows, so its (gloo, host-network) latency is not charged to
+    # the GPU time, and the max over ranks below is the slowest rank's time
+    _lib.check(lib.gm_device_synchronize())
     t_local = time.perf_counter() - t0
+    cp.barrier()
     kernel_ms, launches = sampler.last_run_stats()
     t_max, launch_ms = cp.max([t_local, kernel_ms / max(launches, 1)])
 

@@ -182,6 +182,24 @@ class Sampler:
         _lib.check(self._lib.gm_sampler_set_steps_per_launch(self._h, n))
         return self
 
+    def save_state(self) -> bytes:
+        """Checkpoint (gm_state_save): positions, counters, seed and stream
+        position, NUTS adaptation and metric. The reference has none
+        (core.rs:177 TODO); a sampler restored with load_state continues the
+        same draws bit for bit."""
+        n = C.c_uint64()
+        _lib.check(self._lib.gm_state_size(self._h, C.byref(n)))
+        buf = (C.c_char * n.value)()
+        _lib.check(self._lib.gm_state_save(self._h, buf, n.value))
+        return bytes(buf)
+
+    def load_state(self, blob: bytes):
+        """Resume from save_state's bytes (same sampler kind, dtype, shape and
+        chain offset)."""
+        buf = (C.c_char * len(blob)).from_buffer_copy(blob)
+        _lib.check(self._lib.gm_state_load(self._h, buf, len(blob)))
+        return self
+
     def last_run_stats(self) -> tuple[float, int]:
         ms, n = C.c_double(), C.c_int64()
         _lib.check(self._lib.gm_sampler_last_run_stats(self._h, C.byref(ms), C.byref(n)))

@@ -398,9 +398,11 @@ template <class T> struct GaussT {
   template <int LPC, int E> __host__ __device__ size_t lds_bytes() const {
     return use_lds ? lds_need<LPC, E>(D) : 0;
   }
-  template <int LPC, int E> __device__ __forceinline__ GaussLane<T, LPC, E> bind(int) const {
+  template <int LPC, int E> __device__ __forceinline__ GaussLane<T, LPC, E> bind(int lane) const {
     GaussLane<T, LPC, E> r;
     r.mu = mu;
+#pragma unroll
+    for (int e = 0; e < E; ++e) r.mur[e] = (lane * E + e < D) ? mu[lane * E + e] : (T)0;
     r.prec = prec;
     r.nc = nc;
     r.D = D;
@@ -423,6 +425,7 @@ template <class T> struct GaussT {
 };
 template <class T, int LPC, int E> struct GaussLane {
   const T* mu;
+  T mur[E];  // this lane's mean coordinates (0 past D)
   const T* prec;
   T nc;
   int D;
@@ -435,7 +438,7 @@ template <class T, int LPC, int E> struct GaussLane {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
-      d[e] = (i < D) ? x[e] - mu[i] : (T)0;
+      d[e] = (i < D) ? x[e] - mur[e] : (T)0;
     }
     if (sprec) {
       constexpr int S = LPC * E;

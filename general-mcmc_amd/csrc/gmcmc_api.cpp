@@ -934,6 +934,137 @@ int gm_nuts_get_mass(gm_sampler* s, int32_t* mode, int32_t* kind, void* dinv, vo
   return nuts_get_mass(s->nuts, s->dt, s->C, s->D, kind, dinv, dsqrt, minv, mchol);
 }
 
+// ---- checkpoint / resume ----------------------------------------------------
+// The reference keeps a sampler's state only inside the object across run
+// calls (positions, batched_hmc.rs:40; NUTS epsilon / epsilon_bar / h_bar,
+// generic_nuts.rs:573-582, 744; the metric and the warm-up window schedule);
+// core.rs:177 leaves checkpointing as a TODO. The blob holds exactly that
+// state plus the Philox stream position, so a restored sampler continues bit
+// for bit (runs start at init_chain_state, so NUTS needs no mid-trajectory
+// state; HMC and MH re-evaluate logp at every launch start).
+namespace {
+struct StateHeader {
+  char magic[8];  // "GMCMCST1"
+  int32_t kind, dtype;
+  int64_t C, D;
+  uint64_t seed, step;
+  int64_t total_steps;
+  uint32_t chain_offset;
+  int32_t mass_mode;
+  int64_t m_sb, m_eb, sched_next, sched_len;
+  double m_reg, m_jit;
+};
+struct StatePart {
+  void* dev;
+  size_t bytes;
+};
+std::vector<StatePart> state_parts(gm_sampler* s) {
+  const size_t C = (size_t)s->C, D = (size_t)s->D, e = s->esz;
+  std::vector<StatePart> v{{s->d_q, C * D * e}, {s->d_acc, C * sizeof(long long)}};
+  if (s->kind == K_NUTS) {
+    NutsState& n = s->nuts;
+    v.push_back({n.eps, C * e});
+    v.push_back({n.eps_bar, C * e});
+    v.push_back({n.h_bar, C * e});
+    v.push_back({n.mu, C * e});
+    v.push_back({n.n_leapfrog, C * sizeof(long long)});
+    if (n.mass_mode) {
+      v.push_back({n.mkind, C * sizeof(int)});
+      v.push_back({n.dinv, C * D * e});
+      v.push_back({n.dsq, C * D * e});
+    }
+    if (n.mass_mode == 2) {
+      v.push_back({n.minv, C * D * D * e});
+      v.push_back({n.mchol, C * D * D * e});
+    }
+  }
+  return v;
+}
+size_t state_bytes(gm_sampler* s) {
+  size_t b = sizeof(StateHeader);
+  for (auto& p : state_parts(s)) b += p.bytes;
+  return b;
+}
+}  // namespace
+
+int gm_state_size(gm_sampler* s, uint64_t* bytes) {
+  GM_REQ(s && bytes, "bad arguments");
+  *bytes = state_bytes(s);
+  return GM_OK;
+}
+
+int gm_state_save(gm_sampler* s, void* out, uint64_t bytes) {
+  GM_REQ(s && out, "bad arguments");
+  GM_REQ(bytes >= state_bytes(s), "buffer smaller than gm_state_size");
+  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  StateHeader h;
+  memset(&h, 0, sizeof(h));
+  memcpy(h.magic, "GMCMCST1", 8);
+  h.kind = s->kind;
+  h.dtype = s->dt;
+  h.C = s->C;
+  h.D = s->D;
+  h.seed = s->seed;
+  h.step = s->step;
+  h.total_steps = s->total_steps;
+  h.chain_offset = s->chain_offset;
+  if (s->kind == K_NUTS) {
+    const NutsState& n = s->nuts;
+    h.mass_mode = n.mass_mode;
+    h.m_sb = n.m_sb;
+    h.m_eb = n.m_eb;
+    h.sched_next = n.sched_next;
+    h.sched_len = n.sched_len;
+    h.m_reg = n.m_reg;
+    h.m_jit = n.m_jit;
+  }
+  unsigned char* o = (unsigned char*)out;
+  memcpy(o, &h, sizeof(h));
+  o += sizeof(h);
+  for (auto& p : state_parts(s)) {
+    GM_HIP(hipMemcpy(o, p.dev, p.bytes, hipMemcpyDeviceToHost));
+    o += p.bytes;
+  }
+  return GM_OK;
+}
+
+int gm_state_load(gm_sampler* s, const void* in, uint64_t bytes) {
+  GM_REQ(s && in, "bad arguments");
+  GM_REQ(bytes >= sizeof(StateHeader), "state blob too short");
+  StateHeader h;
+  memcpy(&h, in, sizeof(h));
+  GM_REQ(memcmp(h.magic, "GMCMCST1", 8) == 0, "not a libgmcmc state blob");
+  GM_REQ(h.kind == s->kind && h.dtype == (int32_t)s->dt && h.C == s->C && h.D == s->D &&
+             h.chain_offset == s->chain_offset,
+         "state blob is for a different sampler kind, dtype, shape or chain offset");
+  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  if (s->kind == K_NUTS) {
+    GM_REQ(h.mass_mode >= 0 && h.mass_mode <= 2, "corrupt state blob");
+    if (h.mass_mode != s->nuts.mass_mode || h.mass_mode) {
+      const int rc = nuts_set_mass(&s->nuts, s->dt, s->C, s->D, h.mass_mode, h.m_sb, h.m_eb, 0,
+                                   h.m_reg, h.m_jit);
+      if (rc) return rc;
+    }
+  }
+  // the parts' sizes follow from the (now matching) sampler
+  GM_REQ(bytes >= state_bytes(s), "state blob too short");
+  const unsigned char* p = (const unsigned char*)in + sizeof(h);
+  for (auto& part : state_parts(s)) {
+    GM_HIP(hipMemcpy(part.dev, p, part.bytes, hipMemcpyHostToDevice));
+    p += part.bytes;
+  }
+  s->seed = h.seed;
+  s->step = h.step;
+  s->total_steps = h.total_steps;
+  if (s->kind == K_NUTS) {
+    s->nuts.sched_next = h.sched_next;
+    s->nuts.sched_len = h.sched_len;
+  }
+  return GM_OK;
+}
+
 struct gm_mct {
   long long C = 0;
   int P = 0;

@@ -22,6 +22,8 @@
 // their own control flow. The per-level stack of stored left subtrees lives in
 // global memory laid out [level][field][chain][coordinate]; every lane only
 // ever reads back what it wrote itself, so no cross-lane ordering is needed.
+#include <cstdlib>
+
 #include "gm_layouts.h"
 #include "gm_nuts.h"
 #include "gm_track.h"
@@ -69,6 +71,10 @@ struct NutsLaunch {
   void* rm2d = nullptr;      // [C][D]
   void* rm2 = nullptr;       // [C][D][D] (upper triangle used)
   int* updated = nullptr;    // [C] metric replaced at the previous launch's last step
+  // levels k < lds_levels of the subtree stack live in LDS (after the
+  // target's staging area, at byte offset lds_stack_off), the rest in HBM
+  int lds_levels = 0;
+  unsigned lds_stack_off = 0;
   long long sb = 0, eb = 0;  // start_buffer, end_buffer (should_collect, :153-162)
   int do_refind = 0;         // re-find eps for updated chains first (:905-918)
   uint64_t refind_step = 0;  // transition index of the update (probe draws)
@@ -315,6 +321,71 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   T* __restrict__ salpha = (T*)a.stk_alpha;
   const long long slane = c * LPC + lane;  // scalar-stack slot of this lane
   const long long CL = C * LPC;
+  // Subtree stack. Level k < KL: LDS, [k][field][thread*E + e] vectors and
+  // [k][thread] scalars of this block (a lane reads back only what it wrote:
+  // no synchronisation). Deeper levels: HBM [k][field][chain][coord].
+  constexpr int NT = 256;  // threads per block (launch_nuts)
+  const int KL = a.lds_levels;
+  T* __restrict__ lvec = (T*)(gm_dyn_lds + a.lds_stack_off);
+  T* __restrict__ lalpha = lvec + (long long)KL * 3 * NT * E;
+  int* __restrict__ lnn = (int*)(lalpha + KL * NT);
+  int* __restrict__ lnna = lnn + KL * NT;
+  const int tix = threadIdx.x;
+  auto stack_store = [&](int k, const T (&f0)[E], const T (&f1)[E], const T (&f2)[E], T al, int nn,
+                         int nna) __attribute__((always_inline)) {
+    if (k < KL) {
+      T* v = lvec + (long long)k * 3 * NT * E + tix * E;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        v[e] = f0[e];
+        v[NT * E + e] = f1[e];
+        v[2 * NT * E + e] = f2[e];
+      }
+      lalpha[k * NT + tix] = al;
+      lnn[k * NT + tix] = nn;
+      lnna[k * NT + tix] = nna;
+    } else {
+      T* sv = svec + ((long long)(k * 3) * C + c) * D;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        if (i < D) {
+          sv[i] = f0[e];
+          sv[C * D + i] = f1[e];
+          sv[2 * C * D + i] = f2[e];
+        }
+      }
+      salpha[k * CL + slane] = al;
+      a.stk_n[k * CL + slane] = nn;
+      a.stk_na[k * CL + slane] = nna;
+    }
+  };
+  // field f (0 first q, 1 first p, 2 proposal) of level k
+  auto stack_vec = [&](int k, int f, T (&out)[E]) __attribute__((always_inline)) {
+    if (k < KL) {
+      const T* v = lvec + ((long long)k * 3 + f) * NT * E + tix * E;
+#pragma unroll
+      for (int e = 0; e < E; ++e) out[e] = v[e];
+    } else {
+      const T* sv = svec + ((long long)(k * 3 + f) * C + c) * D;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        out[e] = (i < D) ? sv[i] : (T)0;
+      }
+    }
+  };
+  auto stack_scalars = [&](int k, T& al, long long& nn, long long& nna) __attribute__((always_inline)) {
+    if (k < KL) {
+      al = lalpha[k * NT + tix];
+      nn = lnn[k * NT + tix];
+      nna = lnna[k * NT + tix];
+    } else {
+      al = salpha[k * CL + slane];
+      nn = a.stk_n[k * CL + slane];
+      nna = a.stk_na[k * CL + slane];
+    }
+  };
 
   T q[E];
 #pragma unroll
@@ -460,42 +531,19 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
             // returns it unchanged; going up, it is merged wherever that
             // parent is itself a right child (the recursion's post-order).
             if (!ts) { ++k; continue; }
-            T* sv = svec + ((long long)(k * 3) * C + c) * D;
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-              const int i = lane * E + e;
-              if (i < D) {
-                sv[i] = fq[e];
-                sv[C * D + i] = fp[e];
-                sv[2 * C * D + i] = pr[e];
-              }
-            }
-            salpha[k * CL + slane] = ta;
-            a.stk_n[k * CL + slane] = (int)tn;
-            a.stk_na[k * CL + slane] = (int)tna;
+            stack_store(k, fq, fp, pr, ta, (int)tn, (int)tna);
             break;
           }
           // right child: merge with the stored left sibling (generic_nuts.rs:1251-1323)
-          const T* sv = svec + ((long long)(k * 3) * C + c) * D;
           T lq[E], lpv[E];
-#pragma unroll
-          for (int e = 0; e < E; ++e) {
-            const int i = lane * E + e;
-            lq[e] = (i < D) ? sv[i] : (T)0;
-            lpv[e] = (i < D) ? sv[C * D + i] : (T)0;
-          }
-          const long long ln_ = a.stk_n[k * CL + slane];
-          const long long lna = a.stk_na[k * CL + slane];
-          const T lal = salpha[k * CL + slane];
+          stack_vec(k, 0, lq);
+          stack_vec(k, 1, lpv);
+          long long ln_, lna;
+          T lal;
+          stack_scalars(k, lal, ln_, lna);
           const double u = uniform_co<double>(a.seed, cid, st, TAG_NUTS_MRG, merge_ctr++);
           const long long den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
-          if (!(u < (double)tn / (double)den)) {
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-              const int i = lane * E + e;
-              pr[e] = (i < D) ? sv[2 * C * D + i] : (T)0;
-            }
-          }
+          if (!(u < (double)tn / (double)den)) stack_vec(k, 2, pr);
           tn = ln_ + tn;
           if (ts) ts = (v > 0) ? no_uturn<LPC, E>(lq, qe, lpv, pe) : no_uturn<LPC, E>(qe, lq, pe, lpv);
           ta = lal + ta;
@@ -949,6 +997,16 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
   }
   int pending_refind = 0;
   uint64_t refind_step = 0;
+  // GM_NUTS_LDS_LEVELS caps the LDS stack levels (tests cover both homes)
+  const char* cap_env = getenv("GM_NUTS_LDS_LEVELS");
+  const long long lds_cap = cap_env ? atoll(cap_env) : -1;
+  int ncu = 256;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
+      ncu = 256;
+  }
   for (long long li = 0; li < n_launch; ++li) {
     const long long start = seg_start[li], nst = seg_len[li];
     NutsLaunch a;
@@ -1004,7 +1062,20 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     hipError_t e = dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
       const long long threads = C * LPC;
       const unsigned blocks = (unsigned)((threads + 255) / 256);
-      const size_t lds = t.template lds_bytes<LPC, E>();
+      // LDS: the target's staging area, then as many subtree-stack levels as
+      // fit without costing occupancy (<= 4 blocks of 4 waves per CU by VGPRs)
+      const size_t tgl = (t.template lds_bytes<LPC, E>() + 15) / 16 * 16;
+      const size_t per_level = (size_t)3 * 256 * E * sizeof(T) + (size_t)256 * (sizeof(T) + 8);
+      long long bpc = ((long long)blocks + ncu - 1) / ncu;
+      bpc = bpc < 1 ? 1 : bpc > 4 ? 4 : bpc;
+      size_t budget = (size_t)(160 * 1024) / (size_t)bpc - 1024;
+      if (budget > 64 * 1024) budget = 64 * 1024;
+      long long kl = budget > tgl ? (long long)((budget - tgl) / per_level) : 0;
+      if (kl > a.max_depth) kl = a.max_depth;
+      if (lds_cap >= 0 && kl > lds_cap) kl = lds_cap;
+      a.lds_levels = (int)kl;
+      a.lds_stack_off = (unsigned)tgl;
+      const size_t lds = tgl + (size_t)kl * per_level;
       hipLaunchKernelGGL((nuts_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), lds, st, a, t);
       return hipGetLastError();
     });

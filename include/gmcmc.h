@@ -216,6 +216,18 @@ int gm_sampler_last_run_stats(gm_sampler* s, double* kernel_ms, int64_t* launche
 /* Transitions per kernel launch (state stays in registers inside a launch). */
 int gm_sampler_set_steps_per_launch(gm_sampler* s, int64_t steps);
 
+/* Checkpoint / resume. The reference keeps a sampler's state only in the
+ * object between run calls (batched_hmc.rs:40; generic_nuts.rs:573-582, 744)
+ * and leaves checkpointing as a TODO (core.rs:177). gm_state_save writes that
+ * state (positions, accept / leapfrog counts, seed and stream position; NUTS
+ * step-size adaptation, metric and warm-up schedule) to a caller-owned host
+ * buffer of gm_state_size bytes; gm_state_load restores it into a sampler
+ * created with the same kind, dtype, n_chains, dim and chain_offset, which
+ * then continues the same random streams bit for bit. */
+int gm_state_size(gm_sampler* s, uint64_t* bytes);
+int gm_state_save(gm_sampler* s, void* out, uint64_t bytes);
+int gm_state_load(gm_sampler* s, const void* in, uint64_t bytes);
+
 int gm_destroy(gm_sampler* s);
 
 /* ---- diagnostics (stats.rs) ---------------------------------------------

@@ -109,7 +109,10 @@ def test_mh_samples_bitwise(gm, oracle, dtype, dim, lay):
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("dim,lay", [(2, (2, 1)), (5, (8, 1)), (32, (32, 1)), (32, (16, 2))])
 @pytest.mark.parametrize("progress", [False, True])
-def test_nuts_samples_bitwise(gm, oracle, dtype, dim, lay, progress):
+@pytest.mark.parametrize("lds_levels", [None, "0", "2"])  # subtree stack in LDS / HBM / split
+def test_nuts_samples_bitwise(gm, oracle, dtype, dim, lay, progress, lds_levels, monkeypatch):
+    if lds_levels is not None:
+        monkeypatch.setenv("GM_NUTS_LDS_LEVELS", lds_levels)
     n_chains = 12
     x0 = start(gm, n_chains, dim, dtype, 0.5)
     for name, t in targets(gm, dim):
