@@ -8,8 +8,8 @@ every transition computed by hand-written gfx950 HIP kernels in libgmcmc.so
 from . import _lib, batch_vector
 from ._lib import GMError
 from .core import init, init_det, init_with_seed
-from .distributions import (DenseGaussian, DiffableGaussian2D, Gaussian2D, IsotropicGaussian,
-                            Rosenbrock2D, RosenbrockND)
+from .distributions import (CustomTarget, DenseGaussian, DiffableGaussian2D, Gaussian2D,
+                            IsotropicGaussian, Rosenbrock2D, RosenbrockND)
 from .hmc import HMC
 from .metropolis_hastings import MetropolisHastings
 from .nuts import NUTS, MassMatrix, NUTSChain, NUTSMassMatrixConfig
@@ -18,7 +18,8 @@ from .stats import (BasicStats, ChainStats, MultiChainTracker, Progress, RunStat
 
 __all__ = [
     "HMC", "NUTS", "NUTSChain", "MetropolisHastings", "RosenbrockND", "Rosenbrock2D",
-    "IsotropicGaussian", "DiffableGaussian2D", "DenseGaussian", "Gaussian2D", "init", "init_det",
+    "IsotropicGaussian", "DiffableGaussian2D", "DenseGaussian", "Gaussian2D", "CustomTarget", "init",
+    "init_det",
     "init_with_seed", "split_rhat_mean_ess", "basic_stats", "BasicStats", "RunStats", "GMError",
     "batch_vector", "MultiChainTracker", "ChainStats", "Progress", "NUTSMassMatrixConfig", "MassMatrix",
 ]

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("GMCMC_LIB", os.path.join(_HERE, "lib", "libgmcmc.so")
 
 GM_OK, GM_EINVAL, GM_EHIP, GM_ENOMEM, GM_ERCCL, GM_ESTATE = range(6)
 GM_F32, GM_F64 = 0, 1
-GM_TARGET_ROSENBROCK, GM_TARGET_ISO_GAUSS, GM_TARGET_GAUSS = 1, 2, 3
+GM_TARGET_ROSENBROCK, GM_TARGET_ISO_GAUSS, GM_TARGET_GAUSS, GM_TARGET_CUSTOM = 1, 2, 3, 4
 UNIQUE_ID_BYTES = 128
 
 
@@ -38,6 +38,9 @@ class gm_target(C.Structure):
         ("mean", C.POINTER(C.c_double)),
         ("prec", C.POINTER(C.c_double)),
         ("norm_const", C.c_double),
+        ("source", C.c_char_p),
+        ("params", C.POINTER(C.c_double)),
+        ("n_params", C.c_int64),
     ]
 
 
@@ -65,6 +68,7 @@ SIGNATURES = {
     "gm_gauss_from_cov": (_ip, [_i64, _vp, _vp, _vp]),
     "gm_init_positions": (_ip, [_u64, _i64, _i64, _ip, _vp]),
     "gm_target_logp_grad": (_ip, [C.POINTER(gm_target), _ip, _i64, _vp, _vp, _vp]),
+    "gm_custom_target_check": (_ip, [C.c_char_p, _ip, _i64, _i32]),
     "gm_hmc_create": (_ip, [C.POINTER(gm_target), _ip, _i64, _i64, _vp, _dbl, _i64, _i64, C.POINTER(_vp)]),
     "gm_mh_create": (_ip, [C.POINTER(gm_target), _ip, _i64, _i64, _vp, _dbl, _i64, C.POINTER(_vp)]),
     "gm_nuts_create": (_ip, [C.POINTER(gm_target), _ip, _i64, _i64, _vp, _dbl, _i32, _i64, C.POINTER(_vp)]),

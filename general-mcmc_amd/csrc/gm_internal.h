@@ -7,6 +7,7 @@
 #include <string>
 
 #include "../../include/gmcmc.h"
+#include "gm_launch.h"
 
 namespace gm {
 
@@ -19,6 +20,8 @@ struct TargetDev {
   double a = 1, b = 100, std = 1, norm_const = 0;
   const void* mu = nullptr;    // [D] of the sampler dtype
   const void* prec = nullptr;  // [D*D] of the sampler dtype, transposed (prec[j*D+i] = P_ij)
+  const char* src = nullptr;     // CUSTOM: user source (interned, lives for the process)
+  const void* params = nullptr;  // CUSTOM: [n_params] of the sampler dtype
 };
 
 struct Layout {
@@ -34,38 +37,10 @@ constexpr int GM_WIDE_MAX_DIM = 16384;
 Layout default_layout(int D, gm_dtype dt, int kind);
 
 // ---- HMC -------------------------------------------------------------------
-struct HmcLaunch {
-  void* q = nullptr;            // [C*D] state, in/out
-  void* logp = nullptr;         // [C] out
-  long long* accepts = nullptr; // [C] in/out (+= accepted count)
-  void* samples = nullptr;      // [rows][C][D]
-  long long C = 0;
-  int D = 0;
-  double eps = 0;
-  int L = 0;
-  uint64_t seed = 0;
-  uint64_t step0 = 0;           // global transition index of the first step
-  uint32_t chain_offset = 0;
-  int n_steps = 0;
-  int collect_from = 0;         // steps s >= collect_from are stored ...
-  long long sample_row0 = 0;    // ... at row sample_row0 + (s - collect_from)
-  int lf_unroll = 1;            // leapfrog loop unroll (1 or 4; same results)
-  int stagger = 1;              // per-wave staggered prefetch of the draw blocks (same results)
-  void* zs = nullptr;           // wide layouts: momentum block scratch [C][S][lanes*elems]
-};
 hipError_t launch_hmc(gm_dtype dt, const TargetDev& tg, const Layout& lay, const HmcLaunch& a,
                       hipStream_t st);
 
 // ---- run_progress statistics (gm_track.h, tracker_kernels.hip) -------------
-// Per-chain ChainTracker state (stats.rs:24-131), f32 [C][D] and [C]; mean
-// is null when tracking is off. n0 = tracker steps before this launch.
-struct TrackLaunch {
-  float* mean = nullptr;
-  float* msq = nullptr;
-  float* last = nullptr;
-  float* p = nullptr;
-  unsigned long long n0 = 0;
-};
 // ChainTracker::new for every chain from the current positions
 hipError_t launch_ct_init(gm_dtype dt, long long C, int D, const void* q, const TrackLaunch& t,
                           hipStream_t st);
@@ -81,22 +56,6 @@ hipError_t launch_mct_rhat(long long C, int P, unsigned long long n, const float
                            float* rhat, hipStream_t st);
 
 // ---- MH --------------------------------------------------------------------
-struct MhLaunch {
-  void* q = nullptr;
-  void* logp = nullptr;
-  long long* accepts = nullptr;
-  void* samples = nullptr;
-  long long C = 0;
-  int D = 0;
-  double prop_std = 1;
-  uint64_t seed = 0;
-  uint64_t step0 = 0;
-  uint32_t chain_offset = 0;
-  int n_steps = 0;
-  int collect_from = 0;
-  long long sample_row0 = 0;
-  TrackLaunch trk;              // run_progress chain trackers (off when trk.mean is null)
-};
 hipError_t launch_mh(gm_dtype dt, const TargetDev& tg, const Layout& lay, const MhLaunch& a,
                      hipStream_t st);
 

@@ -1,0 +1,110 @@
+// gm_launch.h — kernel argument blocks (plain structs, device-safe: shared by
+// the AOT kernels, the host launchers and the runtime-compiled user-target
+// kernels of gm_jit.cpp).
+#pragma once
+#include <stdint.h>
+
+namespace gm {
+
+// ---- run_progress statistics (gm_track.h, tracker_kernels.hip) -------------
+// Per-chain ChainTracker state (stats.rs:24-131), f32 [C][D] and [C]; mean
+// is null when tracking is off. n0 = tracker steps before this launch.
+struct TrackLaunch {
+  float* mean = nullptr;
+  float* msq = nullptr;
+  float* last = nullptr;
+  float* p = nullptr;
+  unsigned long long n0 = 0;
+};
+
+// ---- HMC -------------------------------------------------------------------
+struct HmcLaunch {
+  void* q = nullptr;            // [C*D] state, in/out
+  void* logp = nullptr;         // [C] out
+  long long* accepts = nullptr; // [C] in/out (+= accepted count)
+  void* samples = nullptr;      // [rows][C][D]
+  long long C = 0;
+  int D = 0;
+  double eps = 0;
+  int L = 0;
+  uint64_t seed = 0;
+  uint64_t step0 = 0;           // global transition index of the first step
+  uint32_t chain_offset = 0;
+  int n_steps = 0;
+  int collect_from = 0;         // steps s >= collect_from are stored ...
+  long long sample_row0 = 0;    // ... at row sample_row0 + (s - collect_from)
+  int lf_unroll = 1;            // leapfrog loop unroll (1 or 4; same results)
+  int stagger = 1;              // per-wave staggered prefetch of the draw blocks (same results)
+  void* zs = nullptr;           // wide layouts: momentum block scratch [C][S][lanes*elems]
+};
+
+// ---- MH --------------------------------------------------------------------
+struct MhLaunch {
+  void* q = nullptr;
+  void* logp = nullptr;
+  long long* accepts = nullptr;
+  void* samples = nullptr;
+  long long C = 0;
+  int D = 0;
+  double prop_std = 1;
+  uint64_t seed = 0;
+  uint64_t step0 = 0;
+  uint32_t chain_offset = 0;
+  int n_steps = 0;
+  int collect_from = 0;
+  long long sample_row0 = 0;
+  TrackLaunch trk;              // run_progress chain trackers (off when trk.mean is null)
+};
+
+// ---- NUTS ------------------------------------------------------------------
+struct NutsLaunch {
+  void* q = nullptr;
+  long long* accepts = nullptr;
+  long long* n_leapfrog = nullptr;
+  void* samples = nullptr;
+  void* eps = nullptr;
+  void* eps_bar = nullptr;
+  void* h_bar = nullptr;
+  void* mu = nullptr;
+  void* stk_vec = nullptr;
+  void* stk_alpha = nullptr;
+  int* stk_n = nullptr;
+  int* stk_na = nullptr;
+  long long C = 0;
+  int D = 0;
+  int max_depth = 10;
+  double target_accept = 0.8;
+  uint64_t seed = 0;
+  uint64_t step0 = 0;        // global transition index of this launch's first step
+  uint64_t init_step = 0;    // transition counter value used for the init draw
+  uint32_t chain_offset = 0;
+  int n_steps = 0;
+  long long m0 = 0;          // adaptation counter before this launch's first step
+  long long n_discard = 0;
+  int do_init = 0;           // run init_chain_state first (generic_nuts.rs:731-753)
+  long long t0 = 0;          // transitions already done in this run before this launch
+  long long row_shift = 0;   // state after t transitions goes to row t - row_shift
+  long long n_rows = 0;
+  TrackLaunch trk;           // run_progress chain trackers (off when trk.mean is null)
+  // mass-matrix warm-up (generic_nuts.rs:33-359); mass_mode 0 = identity, off
+  int mass_mode = 0;         // 1 diagonal, 2 dense
+  int* mkind = nullptr;      // [C] current metric of each chain: 0 identity, 1 diag, 2 dense
+  void* dinv = nullptr;      // [C][D]
+  void* dsq = nullptr;       // [C][D]
+  void* minv = nullptr;      // [C][D][D]
+  void* mchol = nullptr;     // [C][D][D]
+  int* rn = nullptr;         // [C] RunningCov::n
+  void* rmean = nullptr;     // [C][D]
+  void* rm2d = nullptr;      // [C][D]
+  void* rm2 = nullptr;       // [C][D][D] (upper triangle used)
+  int* updated = nullptr;    // [C] metric replaced at the previous launch's last step
+  // levels k < lds_levels of the subtree stack live in LDS (after the
+  // target's staging area, at byte offset lds_stack_off), the rest in HBM
+  int lds_levels = 0;
+  unsigned lds_stack_off = 0;
+  long long sb = 0, eb = 0;  // start_buffer, end_buffer (should_collect, :153-162)
+  int do_refind = 0;         // re-find eps for updated chains first (:905-918)
+  uint64_t refind_step = 0;  // transition index of the update (probe draws)
+};
+
+}  // namespace gm

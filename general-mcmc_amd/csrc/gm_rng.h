@@ -30,7 +30,9 @@
 #pragma once
 #include <stdint.h>
 
-#if defined(__HIPCC__)
+#if defined(__HIPCC_RTC__)
+#define GM_HD __host__ __device__ __forceinline__
+#elif defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define GM_HD __host__ __device__ __forceinline__
 #else

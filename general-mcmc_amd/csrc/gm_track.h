@@ -6,7 +6,7 @@
 // reference's operation order.
 #pragma once
 #include "gm_device.h"
-#include "gm_internal.h"
+#include "gm_launch.h"
 
 namespace gm {
 

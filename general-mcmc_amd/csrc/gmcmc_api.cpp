@@ -14,10 +14,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <random>
+#include <set>
 #include <string>
 #include <vector>
 
+#include "gm_jit.h"
 #include "gm_layouts.h"
 #include "gm_nuts.h"
 #include "gm_rng.h"
@@ -48,8 +51,12 @@ static int next_pow2(int v) {
 
 Layout default_layout(int D, gm_dtype dt, int kind) {
   (void)dt;
-  (void)kind;
   Layout l;
+  if (kind == GM_TARGET_CUSTOM) {  // user code: one chain per lane
+    l.lanes = 1;
+    l.elems = D;
+    return l;
+  }
   if (D > 1024) {
     // wide: the smallest elems whose workgroup holds the chain, so that a
     // chain gets as many waves as possible (few huge chains fill more of the
@@ -199,6 +206,15 @@ static int ensure_buf(void** p, size_t* cap, size_t need) {
   return GM_OK;
 }
 
+// User sources live as long as the process (kernels compiled from them are
+// cached per process); identical sources share one copy.
+static const char* intern_source(const char* src) {
+  static std::mutex mu;
+  static std::set<std::string> pool;
+  std::lock_guard<std::mutex> lock(mu);
+  return pool.insert(std::string(src)).first->c_str();
+}
+
 // Copy a double array to device as dtype.
 static int upload_as(gm_dtype dt, const double* src, size_t n, void** dst) {
   const size_t esz = dt == GM_F32 ? 4 : 8;
@@ -254,6 +270,19 @@ int gm::build_target(const gm_target* t, gm_dtype dt, long long dim, TargetDev* 
       out->prec = *d_prec;
       break;
     }
+    case GM_TARGET_CUSTOM: {
+      GM_REQ(t->source != nullptr, "CUSTOM needs source");
+      GM_REQ(dim <= GM_CUSTOM_MAX_DIM, "CUSTOM targets support dim <= 256 (one chain per lane)");
+      GM_REQ(t->n_params >= 0 && (t->n_params == 0 || t->params != nullptr), "bad CUSTOM params");
+      out->src = intern_source(t->source);
+      // params (at least one slot, so the pointer is never null)
+      std::vector<double> pv(t->n_params > 0 ? (size_t)t->n_params : 1, 0.0);
+      for (int64_t i = 0; i < t->n_params; ++i) pv[(size_t)i] = t->params[i];
+      int rc = upload_as(dt, pv.data(), pv.size(), d_prec);
+      if (rc) return rc;
+      out->params = *d_prec;
+      break;
+    }
     default:
       GM_REQ(false, "unknown target kind");
   }
@@ -282,6 +311,15 @@ int gm_set_device(int device) {
 int gm_device_synchronize(void) {
   GM_HIP(hipDeviceSynchronize());
   return GM_OK;
+}
+
+int gm_custom_target_check(const char* source, gm_dtype dtype, int64_t dim, int32_t kind) {
+  GM_REQ(source, "source is NULL");
+  GM_REQ(dtype == GM_F32 || dtype == GM_F64, "bad dtype");
+  GM_REQ(dim >= 1 && dim <= GM_CUSTOM_MAX_DIM, "CUSTOM targets support dim in [1, 256]");
+  GM_REQ(kind >= 0 && kind <= 3, "kind: 0 logp/grad, 1 HMC, 2 MH, 3 NUTS");
+  const JitKernel jk = kind == 1 ? JIT_HMC : kind == 2 ? JIT_MH : kind == 3 ? JIT_NUTS : JIT_LOGP;
+  return jit_compile(jk, dtype, source, (int)dim);
 }
 
 // DiffableGaussian2D::new (distributions.rs:229-253); dim > 2 via the
@@ -413,7 +451,18 @@ static int create_common(int kind, const gm_target* target, gm_dtype dtype, int6
     return rc;
   }
   s->lay = default_layout((int)dim, dtype, target->kind);
-  if (kind == K_NUTS && dim > 16 && dim <= 64) {
+  if (target->kind == GM_TARGET_CUSTOM) {
+    // compile the user target into this sampler's kernel now, so that a
+    // source error surfaces here with the compiler log
+    const JitKernel jk = kind == K_HMC ? JIT_HMC : kind == K_MH ? JIT_MH : JIT_NUTS;
+    rc = jit_prepare(jk, dtype, s->tg);
+    if (rc) {
+      const std::string msg = gm_last_error();
+      gm_destroy(s);
+      set_error(msg);
+      return rc;
+    }
+  } else if (kind == K_NUTS && dim > 16 && dim <= 64) {
     // NUTS: two coordinates per lane halve the lanes that wait in each
     // per-chain reduction and put twice the chains in a wave (measured at
     // 8192 x 32-D f64: 1.47x over 32x1 for the dense Gaussian, 1.07x for the
@@ -492,6 +541,9 @@ int gm_sampler_layout(gm_sampler* s, int32_t* lanes, int32_t* elems) {
 
 int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems) {
   GM_REQ(s, "sampler is NULL");
+  GM_REQ(s->tg.kind != GM_TARGET_CUSTOM || (lanes == 1 && elems == s->D),
+         "CUSTOM targets run one chain per lane (layout 1 x dim)");
+  if (s->tg.kind == GM_TARGET_CUSTOM) return GM_OK;
   const bool wide = lanes > 64;
   GM_REQ(wide ? wide_layout_supported(lanes, elems, s->dt) : layout_supported(lanes, elems),
          "layout (lanes, elems) is not compiled in");

@@ -1,0 +1,91 @@
+// mh_device.h — the Metropolis-Hastings transition kernel (device code
+// only; compiled ahead of time by mh_kernels.hip and at run time for user
+// targets by gm_jit.cpp).
+#pragma once
+#include "gm_device.h"
+#include "gm_launch.h"
+#include "gm_track.h"
+
+namespace gm {
+
+template <class T, int LPC, int E, class TG>
+__global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
+  const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long c = gtid / LPC;
+  const int lane = (int)(gtid % LPC);
+  const auto tg = tg_.template bind<LPC, E>(lane);  // per-lane target view
+  if (c >= a.C) return;
+  const int D = a.D;
+  T* __restrict__ qs = (T*)a.q;
+  const uint32_t cid = a.chain_offset + (uint32_t)c;
+  // wave-uniform chain id when one chain fills the wave: the per-chain draws
+  // (accept uniform) then run on the scalar unit
+  const uint32_t ucid = (LPC == 64) ? (uint32_t)__builtin_amdgcn_readfirstlane((int)cid) : cid;
+  const T sd = (T)a.prop_std;
+  const T var = sd * sd;
+  const T two_var = (T)2 * var;
+  const T pi = (T)3.14159265358979323846;
+  const T qconst = (-(T)D * (T)0.5) * glog(((var * pi) * sd) * sd);
+
+  T x[E], y[E], gdummy[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    x[e] = (i < D) ? qs[c * D + i] : (T)0;
+  }
+  T lp = tg.template eval<LPC, E, true>(x, gdummy, lane);
+  long long acc = 0;
+  NormalCache<T> ncache[E];
+  UniformCache<T> ucache;
+  const bool track = a.trk.mean != nullptr;  // run_progress (core.rs:146-163)
+  ChainTrack<LPC, E> tr;
+  if (track) tr.load(a.trk, c, lane, D);
+  for (int s = 0; s < a.n_steps; ++s) {
+    const uint64_t st = a.step0 + (uint64_t)s;
+    T qpart = (T)0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      if (i < D) {
+        const T n = ncache[e].get(a.seed, cid, st, TAG_MH_PROP, (uint32_t)i);
+        y[e] = x[e] + n * sd;
+      } else {
+        y[e] = (T)0;
+      }
+      const T d = y[e] - x[e];
+      const T ex = (i < D) ? (-(d * d)) / two_var : (T)0;
+      qpart = (e == 0) ? ex : qpart + ex;
+    }
+    const T logq = group_sum<LPC>(qpart) + qconst;
+    const T lp1 = tg.template eval<LPC, E, true>(y, gdummy, lane);
+    const T log_alpha = (lp1 + logq) - (lp + logq);
+    const T lnu = glog_unif(ucache.get(a.seed, ucid, st, TAG_MH_ACC, 0u));
+    if (log_alpha > lnu) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) x[e] = y[e];
+      lp = lp1;
+      ++acc;
+    }
+    if (track) tr.step(x, a.trk.n0 + (unsigned long long)s + 1ull, lane, D);
+    if (s >= a.collect_from) {
+      T* __restrict__ out = (T*)a.samples + ((a.sample_row0 + (s - a.collect_from)) * a.C + c) * D;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        if (i < D) out[i] = x[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    if (i < D) qs[c * D + i] = x[e];
+  }
+  if (track) tr.store(a.trk, c, lane, D);
+  if (lane == 0) {
+    ((T*)a.logp)[c] = lp;
+    a.accepts[c] += acc;
+  }
+}
+
+}  // namespace gm

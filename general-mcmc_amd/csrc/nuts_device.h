@@ -1,0 +1,571 @@
+// nuts_device.h — the NUTS transition kernel and its tree / metric helpers
+// (device code only; compiled ahead of time by nuts_kernels.hip and at run
+// time for user targets by gm_jit.cpp). See nuts_kernels.hip for the notes.
+#pragma once
+#include "gm_device.h"
+#include "gm_launch.h"
+#include "gm_track.h"
+
+namespace gm {
+
+
+// coordinate j of a chain's vector: lane j/E of the group, slot j%E
+template <int LPC, int E, class T>
+__device__ __forceinline__ T coord(const T (&x)[E], int j) {
+  const int src = j / E, slot = j % E;
+  T mine = x[0];
+#pragma unroll
+  for (int e = 1; e < E; ++e) mine = (slot == e) ? x[e] : mine;
+  if constexpr (LPC == 1) return mine;
+  else return __shfl(mine, src, LPC);
+}
+
+// MassMatrix (generic_nuts.rs:175-304) of one chain, this lane's view
+template <class T, int E> struct MassDev {
+  int kind = 0;             // 0 identity, 1 diagonal, 2 dense
+  T inv[E], sq[E];          // diagonal
+  const T* minv = nullptr;  // dense [D][D]
+  const T* chol = nullptr;
+  int D = 0;
+};
+
+// inv_mul (:255-273): v = M^-1 p
+template <int LPC, int E, class T>
+__device__ __forceinline__ void inv_mul(const MassDev<T, E>& M, const T (&p)[E], T (&v)[E], int lane) {
+  if (M.kind == 1) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = M.inv[e] * p[e];
+  } else if (M.kind == 2) {
+    T acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = (T)0;
+    for (int j = 0; j < M.D; ++j) {
+      const T pj = coord<LPC, E>(p, j);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        if (i < M.D) acc[e] = acc[e] + M.minv[(long long)i * M.D + j] * pj;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = acc[e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[e] = p[e];
+  }
+}
+
+// sample_momentum (:275-303) applied to standard normals z
+template <int LPC, int E, class T>
+__device__ __forceinline__ void momentum_from(const MassDev<T, E>& M, const T (&z)[E], T (&p)[E], int lane) {
+  if (M.kind == 1) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) p[e] = z[e] * M.sq[e];
+  } else if (M.kind == 2) {
+    T acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = (T)0;
+    for (int j = 0; j < M.D; ++j) {
+      const T zj = coord<LPC, E>(z, j);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        if (i < M.D && j <= i) acc[e] = acc[e] + M.chol[(long long)i * M.D + j] * zj;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) p[e] = acc[e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) p[e] = z[e];
+  }
+}
+
+template <int LPC, int E, class T>
+__device__ __forceinline__ T dot_group(const T (&a)[E], const T (&b)[E]) {
+  T part = a[0] * b[0];
+#pragma unroll
+  for (int e = 1; e < E; ++e) part = part + a[e] * b[e];
+  return group_sum<LPC>(part);
+}
+
+// MassMatrix::kinetic, identity (generic_nuts.rs:230-238): 0.5 * sum p^2
+template <int LPC, int E, class T>
+__device__ __forceinline__ T kinetic(const T (&p)[E]) {
+  return (T)0.5 * dot_group<LPC, E>(p, p);
+}
+
+// leapfrog_with_mass, identity (generic_nuts.rs:1396-1418)
+template <int LPC, int E, class T, class TG>
+__device__ __forceinline__ T leapfrog(const TG& tg, T (&q)[E], T (&p)[E], T (&g)[E], T epsv, int lane) {
+  const T h = epsv * (T)0.5;
+#pragma unroll
+  for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
+#pragma unroll
+  for (int e = 0; e < E; ++e) q[e] = q[e] + p[e] * epsv;
+  const T lp = tg.template eval<LPC, E, true>(q, g, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
+  return lp;
+}
+
+// stop_criterion (generic_nuts.rs:1354-1378), identity mass:
+// (q+ - q-) . p- >= 0  and  (q+ - q-) . p+ >= 0
+template <int LPC, int E, class T>
+__device__ __forceinline__ bool no_uturn(const T (&qm)[E], const T (&qp)[E], const T (&pm)[E],
+                                         const T (&pp)[E]) {
+  T d[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) d[e] = qp[e] - qm[e];
+  const T dm = dot_group<LPC, E>(d, pm);
+  const T dp = dot_group<LPC, E>(d, pp);
+  return dm >= (T)0 && dp >= (T)0;
+}
+
+// MassMatrix::kinetic (:226-253), canonical-order sum of the per-coordinate
+// terms p*p*inv (diagonal) or p_i (M^-1 p)_i (dense)
+template <int LPC, int E, class T>
+__device__ __forceinline__ T kinetic_m(const MassDev<T, E>& M, const T (&p)[E], int lane) {
+  if (M.kind == 0) return kinetic<LPC, E>(p);
+  T t[E];
+  if (M.kind == 1) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) t[e] = p[e] * p[e] * M.inv[e];
+  } else {
+    inv_mul<LPC, E>(M, p, t, lane);
+#pragma unroll
+    for (int e = 0; e < E; ++e) t[e] = p[e] * t[e];
+  }
+  T part = t[0];
+#pragma unroll
+  for (int e = 1; e < E; ++e) part = part + t[e];
+  return (T)0.5 * group_sum<LPC>(part);
+}
+
+// leapfrog_with_mass (:1396-1418): drift by M^-1 p
+template <int LPC, int E, class T, class TG>
+__device__ __forceinline__ T leapfrog_m(const TG& tg, const MassDev<T, E>& M, T (&q)[E], T (&p)[E],
+                                        T (&g)[E], T epsv, int lane) {
+  if (M.kind == 0) return leapfrog<LPC, E>(tg, q, p, g, epsv, lane);
+  const T h = epsv * (T)0.5;
+#pragma unroll
+  for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
+  T v[E];
+  inv_mul<LPC, E>(M, p, v, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) q[e] = q[e] + v[e] * epsv;
+  const T lp = tg.template eval<LPC, E, true>(q, g, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
+  return lp;
+}
+
+// stop_criterion_with_mass (:1354-1378), the top-level U-turn
+template <int LPC, int E, class T>
+__device__ __forceinline__ bool no_uturn_m(const MassDev<T, E>& M, const T (&qm)[E], const T (&qp)[E],
+                                           const T (&pm)[E], const T (&pp)[E], int lane) {
+  if (M.kind == 0) return no_uturn<LPC, E>(qm, qp, pm, pp);
+  T d[E], vm[E], vp[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) d[e] = qp[e] - qm[e];
+  inv_mul<LPC, E>(M, pm, vm, lane);
+  inv_mul<LPC, E>(M, pp, vp, lane);
+  const T dm = dot_group<LPC, E>(d, vm);
+  const T dp = dot_group<LPC, E>(d, vp);
+  return dm >= (T)0 && dp >= (T)0;
+}
+
+template <int LPC, class T>
+__device__ __forceinline__ bool all_finite(const T (&x)[1]) { return true; }
+
+template <int LPC, int E, class T>
+__device__ __forceinline__ bool group_all_finite(const T (&x)[E], int lane, int D) {
+  int bad = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    const T v = x[e];
+    if (i < D && !(v - v == (T)0)) bad = 1;  // inf - inf and NaN - NaN are NaN
+  }
+  return group_sum<LPC>(bad) == 0;
+}
+
+template <class T> __device__ __forceinline__ T rust_min1(T x) {  // T::one().min(x)
+  if (x != x) return (T)1;
+  return x < (T)1 ? x : (T)1;
+}
+
+template <class T> struct MachEps;
+template <> struct MachEps<float> { static constexpr float v = 1.1920928955078125e-07f; };
+template <> struct MachEps<double> { static constexpr double v = 2.220446049250313e-16; };
+
+// find_reasonable_epsilon_with_mass (generic_nuts.rs:1025-1102), identity mass.
+template <int LPC, int E, class T, class TG>
+__device__ T find_reasonable_epsilon(const TG& tg, const T (&q0)[E], const T (&p0)[E], int lane, int D) {
+  const T half = (T)0.5;
+  T eps = (T)1;
+  T g0[E];
+  const T ulogp = tg.template eval<LPC, E, true>(q0, g0, lane);
+  T q[E], p[E], g[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) { q[e] = q0[e]; p[e] = p0[e]; g[e] = g0[e]; }
+  T ulogp1 = leapfrog<LPC, E>(tg, q, p, g, eps, lane);
+  T k = (T)1;
+  for (int it = 0; it < 1100; ++it) {  // bounded: k underflows to 0 long before
+    const bool fin = (ulogp1 - ulogp1 == (T)0) && group_all_finite<LPC, E>(g, lane, D);
+    if (fin) break;
+    k = k * half;
+#pragma unroll
+    for (int e = 0; e < E; ++e) { q[e] = q0[e]; p[e] = p0[e]; g[e] = g0[e]; }
+    ulogp1 = leapfrog<LPC, E>(tg, q, p, g, eps * k, lane);
+  }
+  eps = half * k * eps;
+  const T k0 = kinetic<LPC, E>(p0);
+  T la = ulogp1 - ulogp - (kinetic<LPC, E>(p) - k0);
+  const T a = (la > glog(half)) ? (T)1 : (T)-1;
+  const T ln2 = glog((T)2);
+  for (int it = 0; it < 2200; ++it) {  // bounded (the reference is not)
+    if (!(a * la > -a * ln2)) break;
+    eps = eps * (a > (T)0 ? (T)2 : (T)0.5);  // 2^a, a = +-1
+#pragma unroll
+    for (int e = 0; e < E; ++e) { q[e] = q0[e]; p[e] = p0[e]; g[e] = g0[e]; }
+    ulogp1 = leapfrog<LPC, E>(tg, q, p, g, eps, lane);
+    la = ulogp1 - ulogp - (kinetic<LPC, E>(p) - k0);
+  }
+  return eps;
+}
+
+template <class T, int LPC, int E, class TG>
+__global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
+  const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long c = gtid / LPC;
+  const int lane = (int)(gtid % LPC);
+  const auto tg = tg_.template bind<LPC, E>(lane);  // per-lane target view
+  if (c >= a.C) return;
+  const int D = a.D;
+  const long long C = a.C;
+  const uint32_t cid = a.chain_offset + (uint32_t)c;
+  T* __restrict__ qs = (T*)a.q;
+  T* __restrict__ svec = (T*)a.stk_vec;
+  T* __restrict__ salpha = (T*)a.stk_alpha;
+  const long long slane = c * LPC + lane;  // scalar-stack slot of this lane
+  const long long CL = C * LPC;
+  // Subtree stack. Level k < KL: LDS, [k][field][thread*E + e] vectors and
+  // [k][thread] scalars of this block (a lane reads back only what it wrote:
+  // no synchronisation). Deeper levels: HBM [k][field][chain][coord].
+  constexpr int NT = 256;  // threads per block (launch_nuts)
+  const int KL = a.lds_levels;
+  T* __restrict__ lvec = (T*)(gm_dyn_lds + a.lds_stack_off);
+  T* __restrict__ lalpha = lvec + (long long)KL * 3 * NT * E;
+  int* __restrict__ lnn = (int*)(lalpha + KL * NT);
+  int* __restrict__ lnna = lnn + KL * NT;
+  const int tix = threadIdx.x;
+  auto stack_store = [&](int k, const T (&f0)[E], const T (&f1)[E], const T (&f2)[E], T al, int nn,
+                         int nna) __attribute__((always_inline)) {
+    if (k < KL) {
+      T* v = lvec + (long long)k * 3 * NT * E + tix * E;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        v[e] = f0[e];
+        v[NT * E + e] = f1[e];
+        v[2 * NT * E + e] = f2[e];
+      }
+      lalpha[k * NT + tix] = al;
+      lnn[k * NT + tix] = nn;
+      lnna[k * NT + tix] = nna;
+    } else {
+      T* sv = svec + ((long long)(k * 3) * C + c) * D;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        if (i < D) {
+          sv[i] = f0[e];
+          sv[C * D + i] = f1[e];
+          sv[2 * C * D + i] = f2[e];
+        }
+      }
+      salpha[k * CL + slane] = al;
+      a.stk_n[k * CL + slane] = nn;
+      a.stk_na[k * CL + slane] = nna;
+    }
+  };
+  // field f (0 first q, 1 first p, 2 proposal) of level k
+  auto stack_vec = [&](int k, int f, T (&out)[E]) __attribute__((always_inline)) {
+    if (k < KL) {
+      const T* v = lvec + ((long long)k * 3 + f) * NT * E + tix * E;
+#pragma unroll
+      for (int e = 0; e < E; ++e) out[e] = v[e];
+    } else {
+      const T* sv = svec + ((long long)(k * 3 + f) * C + c) * D;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        out[e] = (i < D) ? sv[i] : (T)0;
+      }
+    }
+  };
+  auto stack_scalars = [&](int k, T& al, long long& nn, long long& nna) __attribute__((always_inline)) {
+    if (k < KL) {
+      al = lalpha[k * NT + tix];
+      nn = lnn[k * NT + tix];
+      nna = lnna[k * NT + tix];
+    } else {
+      al = salpha[k * CL + slane];
+      nn = a.stk_n[k * CL + slane];
+      nna = a.stk_na[k * CL + slane];
+    }
+  };
+
+  T q[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    q[e] = (i < D) ? qs[c * D + i] : (T)0;
+  }
+  T eps = ((T*)a.eps)[c], eps_bar = ((T*)a.eps_bar)[c], h_bar = ((T*)a.h_bar)[c], mu = ((T*)a.mu)[c];
+  const T gamma = (T)0.05, kappa = (T)0.75, delta = (T)a.target_accept;
+  const long long t0c = 10;
+
+  // the chain's metric and warm-up statistics (generic_nuts.rs:33-359)
+  MassDev<T, E> M;
+  M.D = D;
+  int rn = 0;
+  T rmean[E], rm2d[E];
+  if (a.mass_mode) {
+    M.kind = a.mkind[c];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      M.inv[e] = (i < D) ? ((const T*)a.dinv)[c * D + i] : (T)0;
+      M.sq[e] = (i < D) ? ((const T*)a.dsq)[c * D + i] : (T)0;
+      rmean[e] = (i < D) ? ((const T*)a.rmean)[c * D + i] : (T)0;
+      rm2d[e] = (i < D) ? ((const T*)a.rm2d)[c * D + i] : (T)0;
+    }
+    if (a.mass_mode == 2) {
+      M.minv = (const T*)a.minv + (long long)c * D * D;
+      M.chol = (const T*)a.mchol + (long long)c * D * D;
+    }
+    rn = a.rn[c];
+  }
+
+  if (a.do_init) {  // init_chain_state (generic_nuts.rs:731-753)
+    T z[E], p0[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      z[e] = (i < D) ? normal<T>(a.seed, cid, a.init_step, TAG_NUTS_INIT, (uint32_t)i) : (T)0;
+    }
+    momentum_from<LPC, E>(M, z, p0, lane);
+    const T ae = eps + (T)1;
+    if ((ae < (T)0 ? -ae : ae) <= MachEps<T>::v) eps = find_reasonable_epsilon<LPC, E>(tg, q, p0, lane, D);
+    mu = glog((T)10 * eps);
+  }
+  if (a.do_refind && a.updated[c]) {  // after a metric update (generic_nuts.rs:905-918)
+    T z[E], probe[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      z[e] = (i < D) ? normal<T>(a.seed, cid, a.refind_step, TAG_NUTS_PROBE, (uint32_t)i) : (T)0;
+    }
+    momentum_from<LPC, E>(M, z, probe, lane);
+    eps = find_reasonable_epsilon<LPC, E>(tg, q, probe, lane, D);  // identity-mass leapfrog (:1009-1023)
+    mu = glog((T)10 * eps);
+    eps_bar = eps;
+    h_bar = (T)0;
+  }
+  auto record = [&](long long t) {
+    const long long row = t - a.row_shift;
+    if (row >= 0 && row < a.n_rows) {
+      T* __restrict__ out = (T*)a.samples + (row * C + c) * D;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        if (i < D) out[i] = q[e];
+      }
+    }
+  };
+  if (a.t0 == 0) record(0);
+
+  long long acc = 0, nlf = 0;
+  NormalCache<T> ncache[E];
+  const bool track = a.trk.mean != nullptr;  // run_progress (generic_nuts.rs:688-704)
+  ChainTrack<LPC, E> tr;
+  if (track) tr.load(a.trk, c, lane, D);
+  for (int s = 0; s < a.n_steps; ++s) {
+    const uint64_t st = a.step0 + (uint64_t)s;
+    const long long m = a.m0 + s + 1;
+    // --- momentum, slice (generic_nuts.rs:758-768)
+    T p0[E], g0[E];
+    {
+      T z[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        z[e] = (i < D) ? ncache[e].get(a.seed, cid, st, TAG_NUTS_MOM, (uint32_t)i) : (T)0;
+      }
+      momentum_from<LPC, E>(M, z, p0, lane);
+    }
+    const T logp0 = tg.template eval<LPC, E, true>(q, g0, lane);
+    const T joint0 = logp0 - kinetic_m<LPC, E>(M, p0, lane);
+    const T logu = joint0 - exp1<T>(a.seed, cid, st, TAG_NUTS_EXP, 0u);
+    // trajectory ends
+    T qm[E], pm[E], gm_[E], qp[E], pp[E], gp[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      qm[e] = q[e]; qp[e] = q[e];
+      pm[e] = p0[e]; pp[e] = p0[e];
+      gm_[e] = g0[e]; gp[e] = g0[e];
+    }
+    long long n = 1;
+    bool s_ok = true;
+    T alpha = (T)0;
+    long long n_alpha = 0;
+    uint32_t merge_ctr = 0;
+    int j = 0;
+    while (s_ok && j < a.max_depth) {
+      const T u1 = uniform_co<T>(a.seed, cid, st, TAG_NUTS_DIR, (uint32_t)j);
+      const int v = (u1 < (T)0.5) ? 1 : -1;
+      const T epsv = (T)v * eps;
+      // edge state = the trajectory end on side v
+      T qe[E], pe[E], ge[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        qe[e] = v > 0 ? qp[e] : qm[e];
+        pe[e] = v > 0 ? pp[e] : pm[e];
+        ge[e] = v > 0 ? gp[e] : gm_[e];
+      }
+      // current subtree T
+      T fq[E], fp[E], pr[E];
+      long long tn = 0;
+      bool ts = true;
+      T ta = (T)0;
+      long long tna = 0;
+      const long long nleaves = 1LL << j;
+      for (long long l = 0; l < nleaves; ++l) {
+        const T lp = leapfrog_m<LPC, E>(tg, M, qe, pe, ge, epsv, lane);
+        ++nlf;
+        const T joint = lp - kinetic_m<LPC, E>(M, pe, lane);
+        tn = (logu < joint) ? 1 : 0;
+        ts = (logu - (T)1000) < joint;
+        ta = rust_min1(gexp(joint - joint0));
+        tna = 1;
+#pragma unroll
+        for (int e = 0; e < E; ++e) { fq[e] = qe[e]; fp[e] = pe[e]; pr[e] = qe[e]; }
+        bool done = false;
+        int k = 0;
+        while (true) {
+          if (k == j) { done = true; break; }
+          if (((l >> k) & 1) == 0) {  // left child at level k
+            // A truncated left subtree: its parent builds no right half and
+            // returns it unchanged; going up, it is merged wherever that
+            // parent is itself a right child (the recursion's post-order).
+            if (!ts) { ++k; continue; }
+            stack_store(k, fq, fp, pr, ta, (int)tn, (int)tna);
+            break;
+          }
+          // right child: merge with the stored left sibling (generic_nuts.rs:1251-1323)
+          T lq[E], lpv[E];
+          stack_vec(k, 0, lq);
+          stack_vec(k, 1, lpv);
+          long long ln_, lna;
+          T lal;
+          stack_scalars(k, lal, ln_, lna);
+          const double u = uniform_co<double>(a.seed, cid, st, TAG_NUTS_MRG, merge_ctr++);
+          const long long den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
+          if (!(u < (double)tn / (double)den)) stack_vec(k, 2, pr);
+          tn = ln_ + tn;
+          if (ts) ts = (v > 0) ? no_uturn<LPC, E>(lq, qe, lpv, pe) : no_uturn<LPC, E>(qe, lq, pe, lpv);
+          ta = lal + ta;
+          tna = lna + tna;
+#pragma unroll
+          for (int e = 0; e < E; ++e) { fq[e] = lq[e]; fp[e] = lpv[e]; }
+          ++k;
+        }
+        if (done) break;
+      }
+      // the new trajectory end on side v is the last leaf integrated
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (v > 0) { qp[e] = qe[e]; pp[e] = pe[e]; gp[e] = ge[e]; }
+        else { qm[e] = qe[e]; pm[e] = pe[e]; gm_[e] = ge[e]; }
+      }
+      alpha = ta;
+      n_alpha = tna;
+      const T tmp = rust_min1((T)tn / (T)n);
+      const T u2 = uniform_co<T>(a.seed, cid, st, TAG_NUTS_TOP, (uint32_t)j);
+      if (ts && (u2 < tmp)) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) q[e] = pr[e];
+        ++acc;
+      }
+      n += tn;
+      s_ok = ts && no_uturn_m<LPC, E>(M, qm, qp, pm, pp, lane);
+      ++j;
+    }
+    // dual averaging (generic_nuts.rs:882-924)
+    T eta = (T)1 / (T)(m + t0c);
+    h_bar = ((T)1 - eta) * h_bar + eta * (delta - alpha / (T)n_alpha);
+    if (m <= a.n_discard) {
+      const T mf = (T)m;
+      eps = gexp(mu - gsqrt(mf) / gamma * h_bar);
+      eta = gexp(-kappa * glog(mf));  // m^(-kappa)
+      eps_bar = gexp(((T)1 - eta) * glog(eps_bar) + eta * glog(eps));
+      // RunningCov::update inside the collection window (:897-903, 108-129)
+      const long long lim = a.n_discard > a.eb ? a.n_discard - a.eb : 0;
+      if (a.mass_mode && m > a.sb && m < lim) {
+        rn += 1;
+        const T ns = (T)rn;
+        T d1[E], d2[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          d1[e] = q[e] - rmean[e];
+          rmean[e] = rmean[e] + d1[e] / ns;
+          d2[e] = q[e] - rmean[e];
+          rm2d[e] = rm2d[e] + d1[e] * d2[e];
+        }
+        if (a.mass_mode == 2) {
+          T* m2 = (T*)a.rm2 + (long long)c * D * D;
+          for (int jj = 0; jj < D; ++jj) {
+            const T dj = coord<LPC, E>(d2, jj);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+              const int i = lane * E + e;
+              if (i < D && jj >= i) m2[(long long)i * D + jj] = m2[(long long)i * D + jj] + d1[e] * dj;
+            }
+          }
+        }
+      }
+    } else {
+      eps = eps_bar;
+    }
+    if (track) tr.step(q, a.trk.n0 + (unsigned long long)s + 1ull, lane, D);
+    record(a.t0 + s + 1);
+  }
+  if (track) tr.store(a.trk, c, lane, D);
+  if (a.mass_mode) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      if (i < D) {
+        ((T*)a.rmean)[c * D + i] = rmean[e];
+        ((T*)a.rm2d)[c * D + i] = rm2d[e];
+      }
+    }
+    if (lane == 0) a.rn[c] = rn;
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    if (i < D) qs[c * D + i] = q[e];
+  }
+  if (lane == 0) {
+    ((T*)a.eps)[c] = eps;
+    ((T*)a.eps_bar)[c] = eps_bar;
+    ((T*)a.h_bar)[c] = h_bar;
+    ((T*)a.mu)[c] = mu;
+    a.accepts[c] += acc;
+    a.n_leapfrog[c] += nlf;
+  }
+}
+
+}  // namespace gm

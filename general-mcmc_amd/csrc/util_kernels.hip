@@ -2,35 +2,11 @@
 // points, batched_hmc.rs:18-22 / hmc.rs:42-61) and the sample-layout
 // transpose used on egress ([N][C][D] device -> [C][N][D] reference layout,
 // hmc.rs:179-180).
+#include "util_device.h"
+#include "gm_jit.h"
 #include "gm_layouts.h"
 
 namespace gm {
-
-template <class T, int LPC, int E, class TG>
-__global__ __launch_bounds__(256) void logp_grad_kernel(long long n, int D, const T* __restrict__ x,
-                                                        T* __restrict__ logp, T* __restrict__ grad,
-                                                        TG tg_) {
-  const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long c = gtid / LPC;
-  const int lane = (int)(gtid % LPC);
-  const auto tg = tg_.template bind<LPC, E>(lane);  // per-lane target view
-  if (c >= n) return;
-  T q[E], g[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int i = lane * E + e;
-    q[e] = (i < D) ? x[c * D + i] : (T)0;
-  }
-  const T lp = tg.template eval<LPC, E, true>(q, g, lane);
-  if (grad) {
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int i = lane * E + e;
-      if (i < D) grad[c * D + i] = g[e];
-    }
-  }
-  if (lane == 0 && logp) logp[c] = lp;
-}
 
 // dim > 1024: one point per workgroup (the wide layout of hmc_wide_kernel)
 template <class T, int E, class TG>
@@ -61,6 +37,15 @@ __global__ __launch_bounds__(gm_wide_max_threads(sizeof(T), E)) void logp_grad_w
 
 hipError_t launch_logp_grad(gm_dtype dt, const TargetDev& tg, const Layout& lay, long long n,
                             const void* x, void* logp, void* grad, hipStream_t st) {
+  if (tg.kind == GM_TARGET_CUSTOM) {  // user target, runtime-compiled (gm_jit.cpp)
+    long long nn = n;
+    int D = tg.D;
+    const void* xx = x;
+    void *lp = logp, *gr = grad;
+    UserTargetArg ut{tg.params, tg.D};
+    void* args[] = {&nn, &D, &xx, &lp, &gr, &ut};
+    return jit_launch(JIT_LOGP, dt, tg, (unsigned)((n + 255) / 256), 256, 0, st, args);
+  }
   if (layout_is_wide(lay)) {
     if (n == 0) return hipSuccess;
     return dispatch_wide(dt, tg, lay, [&]<class T, int E, class TG>(TG t) -> hipError_t {

@@ -10,6 +10,9 @@ log-density with an analytic gradient (no autodiff graph, hmc.rs:42-61).
     DiffableGaussian2D    distributions.rs:215-320
     DenseGaussian         DiffableGaussian2D generalised to dim D
     Gaussian2D            distributions.rs:161-208   (Target, no norm const)
+    CustomTarget          a user target (the Target / GradientTarget traits,
+                          distributions.rs:67-110) as HIP source, compiled at
+                          run time into the sampler kernels
 """
 from __future__ import annotations
 
@@ -170,3 +173,44 @@ class Gaussian2D(_GaussBase):
         det = c[0, 0] * c[1, 1] - c[0, 1] * c[1, 0]
         return float(self.unnorm_logp(np.asarray(position, dtype=np.float64))) + (
             -math.log(2.0 * math.pi) - 0.5 * math.log(abs(det)))
+
+
+class CustomTarget(_TargetBase):
+    """A user-defined target, the counterpart of implementing the reference's
+    GradientTarget / BatchedGradientTarget traits (distributions.rs:67-110).
+
+    `source` is HIP C++ defining, for T = float and double,
+
+        template <class T>
+        __device__ T gm_logp_grad(const T* x, T* g, const T* params);
+
+    which receives one chain's position x[GM_DIM] (GM_DIM is a macro equal to
+    `dim`), writes the gradient of the unnormalised log-density to g[GM_DIM]
+    and returns the log-density. `params` are copied to the device in the
+    sampler's dtype. The source is compiled at run time (hiprtc) together
+    with the engine's own HMC / MH / NUTS kernels, one chain per lane
+    (layout 1 x dim, dim <= 256); a compile error raises at sampler creation
+    with the compiler log. The gradient is the user's: there is no autodiff
+    on the device."""
+
+    def __init__(self, source: str, dim: int, params=()):
+        self.source = str(source)
+        self.dim = int(dim)
+        self.params = np.ascontiguousarray(np.asarray(params, dtype=np.float64).reshape(-1))
+
+    def _fill(self, t, dim):
+        t.kind = _lib.GM_TARGET_CUSTOM
+        src = self.source.encode()
+        t.source = src
+        t.params = self.params.ctypes.data_as(C.POINTER(C.c_double))
+        t.n_params = self.params.size
+        return [src, self.params]
+
+    _KINDS = {"logp": 0, "hmc": 1, "mh": 2, "nuts": 3}
+
+    def check(self, sampler: str = "hmc", dtype=np.float64) -> None:
+        """Compile the source into `sampler`'s kernel ("hmc", "mh", "nuts" or
+        "logp") without running it; raises GMError with the compiler log."""
+        lib = _lib.load()
+        _lib.check(lib.gm_custom_target_check(self.source.encode(), _lib.dtype_code(dtype), self.dim,
+                                              self._KINDS[sampler]))

@@ -54,10 +54,17 @@ typedef enum gm_target_kind {
   GM_TARGET_ROSENBROCK = 1, /* RosenbrockND (a=1,b=100) distributions.rs:535-555;
                                Rosenbrock2D{a,b} distributions.rs:495-530    */
   GM_TARGET_ISO_GAUSS = 2,  /* IsotropicGaussian as Target, distributions.rs:398-406 */
-  GM_TARGET_GAUSS = 3       /* DiffableGaussian2D distributions.rs:215-320 generalised
+  GM_TARGET_GAUSS = 3,      /* DiffableGaussian2D distributions.rs:215-320 generalised
                                to D dims: logp = norm_const - 0.5 (x-mu)^T P (x-mu),
                                P = Sigma^-1 supplied row-major; also Gaussian2D as a
                                Target (distributions.rs:193-207) with norm_const = 0 */
+  GM_TARGET_CUSTOM = 4      /* user code (the reference's Target / GradientTarget
+                               traits, distributions.rs:67-110): HIP source defining
+                                 template <class T> __device__
+                                 T gm_logp_grad(const T* x, T* g, const T* params);
+                               for one chain (x, g of length GM_DIM, a macro = dim),
+                               compiled at run time (hiprtc) into the sampler kernels;
+                               one chain per lane, dim <= 256 */
 } gm_target_kind;
 
 typedef struct gm_target {
@@ -69,7 +76,15 @@ typedef struct gm_target {
   const double* mean;    /* GAUSS: [dim] */
   const double* prec;    /* GAUSS: [dim*dim] row-major inverse covariance */
   double norm_const;     /* GAUSS: additive constant */
+  const char* source;    /* CUSTOM: HIP source of gm_logp_grad (copied) */
+  const double* params;  /* CUSTOM: [n_params] copied to the device in the sampler dtype */
+  int64_t n_params;      /* CUSTOM: passed to gm_logp_grad as `params` */
 } gm_target;
+
+/* Compile a CUSTOM target's source for the sampler kernels without running it
+ * (kind: 1 HMC, 2 MH, 3 NUTS, 0 log-density/gradient); GM_EINVAL with the
+ * compiler log in gm_last_error() when it does not compile. */
+int gm_custom_target_check(const char* source, gm_dtype dtype, int64_t dim, int32_t kind);
 
 /* DiffableGaussian2D::new (distributions.rs:229-253) generalised: from a mean
  * and covariance compute the precision matrix and norm_const =
