@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -37,21 +38,39 @@ using namespace gm;
   } while (0)
 
 namespace {
+// Device buffers of the diagnostics, kept per (host thread, device) and only
+// grown: a call then costs its kernels and copies, not hipMalloc/hipFree
+// (hipFree synchronises the device). Never freed (process lifetime).
 struct DevBuf {
   void* p = nullptr;
-  ~DevBuf() {
-    if (p) hipFree(p);
-  }
+  size_t cap = 0;
   int alloc(size_t n) {
     if (n == 0) n = 8;
+    if (cap >= n) return GM_OK;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
     if (hipMalloc(&p, n) != hipSuccess) {
       p = nullptr;
       set_error("device allocation failed in diagnostics");
       return GM_ENOMEM;
     }
+    cap = n;
     return GM_OK;
   }
 };
+struct DiagBufs {
+  DevBuf cm, s2, ac, cm_all, s2_all, ac_all, out, cnt, cnt_all;
+  DiagScratch ws;
+};
+DiagBufs& diag_bufs() {
+  static thread_local std::map<int, DiagBufs*> per_device;
+  int dev = 0;
+  hipGetDevice(&dev);
+  DiagBufs*& b = per_device[dev];
+  if (!b) b = new DiagBufs();
+  return *b;
+}
 }  // namespace
 
 struct gm_comm {
@@ -71,19 +90,21 @@ static int local_diag(const void* dev_sample, gm_dtype dtype, int64_t C, int64_t
   const int h = (int)(N / 2);
   const int R = comm ? comm->nranks : 1;
   // local products
-  DevBuf cm, s2, ac, cm_all, s2_all, ac_all, out;
+  DiagBufs& B = diag_bufs();
+  DevBuf &cm = B.cm, &s2 = B.s2, &ac = B.ac, &cm_all = B.cm_all, &s2_all = B.s2_all,
+         &ac_all = B.ac_all, &out = B.out;
+  DiagScratch& ws = B.ws;
   int rc;
   if ((rc = cm.alloc(sizeof(double) * 2 * C * P)) || (rc = s2.alloc(sizeof(double) * 2 * C * P)) ||
       (rc = ac.alloc(sizeof(double) * h * P)) || (rc = out.alloc(sizeof(float) * 2 * P)))
     return rc;
-  DiagScratch ws;
   rc = diag_series(dtype, dev_sample, C, N, P, sc, sd, sp, (double*)cm.p, (double*)s2.p,
                    (double*)ac.p, ws, st);
   if (rc) return rc;
   const double *pcm = (double*)cm.p, *ps2 = (double*)s2.p, *pac = (double*)ac.p;
   if (R > 1) {
     // all ranks must hold equally many chains (contiguous equal shards)
-    DevBuf cnt, cnt_all;
+    DevBuf &cnt = B.cnt, &cnt_all = B.cnt_all;
     if ((rc = cnt.alloc(sizeof(long long))) || (rc = cnt_all.alloc(sizeof(long long) * R))) return rc;
     long long c64 = C;
     GM_HIP(hipMemcpyAsync(cnt.p, &c64, sizeof(long long), hipMemcpyHostToDevice, st));
@@ -141,12 +162,21 @@ int gm_split_rhat_ess(const void* sample, gm_dtype dtype, int64_t n_chains, int6
          "need n_chains >= 1, n_draws >= 2, n_params >= 1");
   const size_t esz = dtype == GM_F32 ? 4 : 8;
   const size_t bytes = (size_t)n_chains * n_draws * n_params * esz;
-  DevBuf d;
-  int rc = d.alloc(bytes);
-  if (rc) return rc;
-  GM_HIP(hipMemcpy(d.p, sample, bytes, hipMemcpyHostToDevice));
-  return local_diag(d.p, dtype, n_chains, n_draws, n_params, n_draws * n_params, n_params, 1,
-                    nullptr, rhat_out, ess_out, nullptr);
+  void* d = nullptr;  // the host sample's device copy lives for this call only
+  if (hipMalloc(&d, bytes) != hipSuccess) {
+    set_error("device allocation failed in diagnostics");
+    return GM_ENOMEM;
+  }
+  int rc = GM_OK;
+  if (hipMemcpy(d, sample, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+    set_error("copying the sample to the device failed");
+    rc = GM_EHIP;
+  } else {
+    rc = local_diag(d, dtype, n_chains, n_draws, n_params, n_draws * n_params, n_params, 1, nullptr,
+                    rhat_out, ess_out, nullptr);
+  }
+  hipFree(d);
+  return rc;
 }
 
 int gm_comm_get_unique_id(void* id_out) {
