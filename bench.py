@@ -75,6 +75,8 @@ def main():
         _lib.check(lib.gm_device_synchronize())
         cp.barrier()
 
+    # the sample buffer is resident before the clock starts, like the state
+    sampler.reserve(a.steps)
     # warmup = burn-in transitions (untimed)
     if a.warmup > 0:
         sampler.run_positions(0, a.warmup)

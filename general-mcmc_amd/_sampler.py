@@ -178,6 +178,12 @@ class Sampler:
         _lib.check(self._lib.gm_sampler_set_layout(self._h, lanes, elems))
         return self
 
+    def reserve(self, n_collect: int):
+        """Pre-size the device sample buffer for runs of up to n_collect
+        collected transitions (no allocation inside those runs)."""
+        _lib.check(self._lib.gm_sampler_reserve(self._h, n_collect))
+        return self
+
     def set_steps_per_launch(self, n: int):
         _lib.check(self._lib.gm_sampler_set_steps_per_launch(self._h, n))
         return self

@@ -564,6 +564,13 @@ int gm_sampler_set_steps_per_launch(gm_sampler* s, int64_t steps) {
   return GM_OK;
 }
 
+int gm_sampler_reserve(gm_sampler* s, int64_t n_collect) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(n_collect >= 0, "n_collect must be >= 0");
+  GM_HIP(hipSetDevice(s->device));
+  return ensure_buf(&s->d_samples, &s->samples_bytes, (size_t)n_collect * s->C * s->D * s->esz);
+}
+
 int gm_sampler_last_run_stats(gm_sampler* s, double* kernel_ms, int64_t* launches) {
   GM_REQ(s, "sampler is NULL");
   if (kernel_ms) *kernel_ms = s->last_ms;

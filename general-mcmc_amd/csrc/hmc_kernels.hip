@@ -16,6 +16,7 @@
 // The gradient at the current point is carried across transitions (the
 // reference re-evaluates it twice per step, batched_hmc.rs:138,169; same
 // values), so a transition costs exactly L target evaluations.
+#include <stdlib.h>
 #include "hmc_device.h"
 #include "gm_jit.h"
 #include "gm_layouts.h"
@@ -38,7 +39,8 @@ hipError_t launch_hmc(gm_dtype dt, const TargetDev& tg, const Layout& lay, const
   return dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
     const long long threads = a.C * LPC;
     const unsigned blocks = (unsigned)((threads + 255) / 256);
-    const size_t lds = t.template lds_bytes<LPC, E>();
+    size_t lds = t.template lds_bytes<LPC, E>();
+    if (const char* v = getenv("GM_HMC_LDS_PAD")) lds += (size_t)atol(v);  // measurement knob
     hipLaunchKernelGGL((hmc_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), lds, st, a, t);
     return hipGetLastError();
   });

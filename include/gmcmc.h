@@ -231,6 +231,12 @@ int gm_sampler_last_run_stats(gm_sampler* s, double* kernel_ms, int64_t* launche
 /* Transitions per kernel launch (state stays in registers inside a launch). */
 int gm_sampler_set_steps_per_launch(gm_sampler* s, int64_t steps);
 
+/* Pre-size the device sample buffer for runs collecting up to n_collect
+ * transitions, so that a later gm_run / gm_run_device does no device
+ * allocation (the buffer only grows; hmc.rs:164-181 allocates its output on
+ * every run). */
+int gm_sampler_reserve(gm_sampler* s, int64_t n_collect);
+
 /* Checkpoint / resume. The reference keeps a sampler's state only in the
  * object between run calls (batched_hmc.rs:40; generic_nuts.rs:573-582, 744)
  * and leaves checkpointing as a TODO (core.rs:177). gm_state_save writes that
