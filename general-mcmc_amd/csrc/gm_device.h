@@ -163,6 +163,10 @@ template <class T> __device__ __forceinline__ T keep(T v, typename MaskOf<T>::ty
 //   g_i = A_i - B_i,  A_i = [i<=D-2] ( (4b x_i) t_i + 2 (a - x_i) ),
 //                     B_i = [1<=i<=D-1] (2b t_{i-1}),   t_i = x_{i+1} - x_i^2
 // ([.] selects +0 when false).
+// explicit fused multiply-add (one rounding; C fma/fmaf in the oracle)
+__device__ __forceinline__ float gfma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double gfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
 template <class T, int E> struct RosenbrockLane;
 template <class T> struct RosenbrockT {
   T a, b, b2, b4;  // b2 = 2b, b4 = 4b (rounded once, host side)
@@ -178,8 +182,9 @@ template <class T> struct RosenbrockT {
       r.ms[e] = lane_mask<T>(i <= D - 2);
       r.mp[e] = lane_mask<T>((i >= 1) & (i <= D - 1));
       r.b4m[e] = (i <= D - 2) ? b4 : (T)0;
-      r.c2m[e] = (i <= D - 2) ? (T)2 : (T)0;
-      r.b2m[e] = ((i >= 1) & (i <= D - 1)) ? b2 : (T)0;
+      r.nc2m[e] = (i <= D - 2) ? (T)-2 : (T)0;
+      r.cam[e] = (i <= D - 2) ? (T)2 * a : (T)0;
+      r.nb2m[e] = ((i >= 1) & (i <= D - 1)) ? -b2 : (T)0;
     }
     return r;
   }
@@ -188,7 +193,7 @@ template <class T, int E> struct RosenbrockLane {
   T a, b, b2, b4;
   int Dc;
   typename MaskOf<T>::type ms[E], mp[E];  // [i <= D-2], [1 <= i <= D-1]
-  T b4m[E], c2m[E], b2m[E];               // 4b, 2, 2b where those masks hold, else 0
+  T b4m[E], nc2m[E], cam[E], nb2m[E];     // 4b, -2, 2a, -2b where those masks hold, else 0
   template <int LPC, int E_, bool LOGP>
   __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int) const {
     static_assert(E_ == E, "layout mismatch");
@@ -215,11 +220,10 @@ template <class T, int E> struct RosenbrockLane {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const T tprev = (e > 0) ? t[(e > 0) ? e - 1 : 0] : tp;
-        const T am = a - x[e];
-        const T A = (b4m[e] * x[e]) * t[e] + c2m[e] * am;
-        const T B = b2m[e] * tprev;
-        g[e] = A - B;
+        // g = x (4b t - 2) + 2a - 2b t_prev as three fused multiply-adds
+        g[e] = gfma(nb2m[e], tprev, gfma(x[e], gfma(b4m[e], t[e], nc2m[e]), cam[e]));
         if (LOGP) {
+          const T am = a - x[e];
           const T s = keep(b * (t[e] * t[e]) + am * am, ms[e]);
           part = (e == 0) ? s : part + s;
         }
@@ -287,11 +291,9 @@ template <class T, int E> struct RosenbrockLane {
       for (int e = 0; e < E; ++e) {
         const T xn = (e + 1 < E) ? x[(e + 1 < E) ? e + 1 : e] : nx;
         const T te = xn - x[e] * x[e];
-        const T am = a - x[e];
-        const T A = (b4 * x[e]) * te + (T)2 * am;
-        const T B = b2 * tprev;
-        g[e] = A - B;
+        g[e] = gfma(-b2, tprev, gfma(x[e], gfma(b4, te, (T)-2), (T)2 * a));
         if (LOGP) {
+          const T am = a - x[e];
           const T s = b * (te * te) + am * am;
           part = (e == 0) ? s : part + s;
         }
@@ -308,11 +310,9 @@ template <class T, int E> struct RosenbrockLane {
         const bool hs = i <= Dv - 2, hp = (i >= 1) & (i <= Dv - 1);
         const T xn = (e + 1 < E) ? x[(e + 1 < E) ? e + 1 : e] : nx;
         const T te = xn - x[e] * x[e];
-        const T am = a - x[e];
-        const T A = ((hs ? b4 : (T)0) * x[e]) * te + (hs ? (T)2 : (T)0) * am;
-        const T B = (hp ? b2 : (T)0) * tprev;
-        g[e] = A - B;
+        g[e] = gfma(hp ? -b2 : (T)0, tprev, gfma(x[e], gfma(hs ? b4 : (T)0, te, hs ? (T)-2 : (T)0), hs ? (T)2 * a : (T)0));
         if (LOGP) {
+          const T am = a - x[e];
           const T s = hs ? b * (te * te) + am * am : (T)0;
           part = (e == 0) ? s : part + s;
         }
@@ -381,8 +381,6 @@ template <class T> struct IsoGaussT {
 extern __shared__ __attribute__((aligned(16))) unsigned char gm_dyn_lds[];
 
 // fused multiply-add, one rounding (the oracle's FMA)
-__device__ __forceinline__ float gfma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-__device__ __forceinline__ double gfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
 template <class T, int LPC, int E> struct GaussLane;
 template <class T> struct GaussT {
