@@ -6,7 +6,7 @@ set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 SRC=$1; OUT=$2
 mkdir -p "$OUT"
-FLAGS="--offload-arch=gfx950 -O3 -std=c++20 -ffp-contract=off -fno-slp-vectorize -fPIC -I/opt/rocm/include -I$SRC/../include"
+FLAGS="$AB_DEFS --offload-arch=gfx950 -O3 -std=c++20 -ffp-contract=off -fno-slp-vectorize -fPIC -I/opt/rocm/include -I$SRC/../include"
 /opt/rocm/bin/hipcc $FLAGS -c "$SRC/hmc_kernels.hip" -o "$OUT/hmc_kernels.hip.o"
 B=$ROOT/general-mcmc_amd/build
 OBJS=$(ls $B/*.o | grep -v hmc_kernels)
