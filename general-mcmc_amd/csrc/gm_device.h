@@ -98,6 +98,32 @@ template <int LPC, class T> __device__ __forceinline__ T group_sum(T v) {
   }
   return v;
 }
+// N independent group sums, stage-major: the same stages (and bits) as N
+// calls of group_sum, issued interleaved so that each DPP stage's latency is
+// covered by the other sums' stages instead of wait states.
+// X without const (no <type_traits> under the runtime compiler)
+template <class X> struct Bare { using type = X; };
+template <class X> struct Bare<const X> { using type = X; };
+
+template <int LPC, int N, class T> __device__ __forceinline__ void group_sum_n(T (&v)[N]) {
+  // sched_barrier(0) between stages keeps the machine scheduler from
+  // regrouping the stages per sum (it does, without them)
+#define GM_STAGE(COND, EXPR)                                  \
+  if constexpr (COND) {                                       \
+    __builtin_amdgcn_sched_barrier(0);                        \
+    _Pragma("unroll") for (int k = 0; k < N; ++k) v[k] = EXPR; \
+  }
+  GM_STAGE(LPC >= 2, v[k] + dpp<DPP_QUAD_XOR1>(v[k]))
+  GM_STAGE(LPC >= 4, v[k] + dpp<DPP_QUAD_XOR2>(v[k]))
+  GM_STAGE(LPC >= 8, v[k] + dpp<DPP_ROW_HALF_MIRROR>(v[k]))
+  GM_STAGE(LPC >= 16, v[k] + dpp<DPP_ROW_MIRROR>(v[k]))
+  GM_STAGE(LPC == 32, v[k] + __shfl_xor(v[k], 16, 64))
+  GM_STAGE(LPC >= 64, v[k] + (dpp_rows<DPP_ROW_BCAST15, 0xa>(v[k])))
+  GM_STAGE(LPC >= 64, v[k] + (dpp_rows<DPP_ROW_BCAST31, 0x8>(v[k])))
+  GM_STAGE(LPC >= 64, lane63(v[k]))
+#undef GM_STAGE
+  __builtin_amdgcn_sched_barrier(0);
+}
 // lane l receives lane l+1's value. Wave-wide DPP shift: at a group's last
 // lane the value comes from the next group (or 0); callers mask it, since a
 // group's last coordinate never has a successor inside the chain.
@@ -198,36 +224,7 @@ template <class T, int E> struct RosenbrockLane {
   __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int) const {
     static_assert(E_ == E, "layout mismatch");
     if constexpr (LPC == 64) {
-      // One chain per wave: the lane shifts read 0 beyond the wave and the
-      // padding coordinates are 0, so a boundary lane can only see finite
-      // values of its own chain. The [.] factors are then applied by
-      // multiplying with per-lane constants that are 0 where the term is
-      // absent (the engine's canonical form for 64-lane groups; the oracle
-      // mirrors it), and (x_{i-1})^2 is shifted in from the lane that
-      // computed it, so t_{i-1} is one DPP-fed subtract.
-      T xx[E], t[E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) xx[e] = x[e] * x[e];
-      const T nx = from_next<LPC>(x[0]);
-      const T pxx = from_prev<LPC>(xx[E - 1]);
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const T xn = (e + 1 < E) ? x[(e + 1 < E) ? e + 1 : e] : nx;
-        t[e] = xn - xx[e];
-      }
-      const T tp = x[0] - pxx;
-      T part = (T)0;
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const T tprev = (e > 0) ? t[(e > 0) ? e - 1 : 0] : tp;
-        // g = x (4b t - 2) + 2a - 2b t_prev as three fused multiply-adds
-        g[e] = gfma(nb2m[e], tprev, gfma(x[e], gfma(b4m[e], t[e], nc2m[e]), cam[e]));
-        if (LOGP) {
-          const T am = a - x[e];
-          const T s = keep(b * (t[e] * t[e]) + am * am, ms[e]);
-          part = (e == 0) ? s : part + s;
-        }
-      }
+      const T part = eval64<LOGP>(x, g);
       if (LOGP) return -group_sum<LPC>(part);
       return (T)0;
     }
@@ -259,7 +256,54 @@ template <class T, int E> struct RosenbrockLane {
     if (LOGP) return -group_sum<LPC>(part);
     return (T)0;
   }
-  // The 64-lane form above for a chain spread over a workgroup: the wave-
+  // The 64-lane form split for callers that reduce the log-density together
+  // with another per-chain sum (hmc_kernel's last leapfrog): eval_part
+  // returns this lane's unreduced term, logp = finish(group_sum(part)).
+  template <int LPC> static constexpr bool has_part = (LPC == 64);
+  template <int LPC, int E_>
+  __device__ __forceinline__ T eval_part(const T (&x)[E], T (&g)[E], int) const {
+    static_assert(E_ == E && LPC == 64, "64-lane form only");
+    return eval64<true>(x, g);
+  }
+  __device__ __forceinline__ T finish(T total) const { return -total; }
+  template <bool LOGP>
+  __device__ __forceinline__ T eval64(const T (&x)[E], T (&g)[E]) const {
+    constexpr int LPC = 64;
+    {
+      // One chain per wave: the lane shifts read 0 beyond the wave and the
+      // padding coordinates are 0, so a boundary lane can only see finite
+      // values of its own chain. The [.] factors are then applied by
+      // multiplying with per-lane constants that are 0 where the term is
+      // absent (the engine's canonical form for 64-lane groups; the oracle
+      // mirrors it), and (x_{i-1})^2 is shifted in from the lane that
+      // computed it, so t_{i-1} is one DPP-fed subtract.
+      T xx[E], t[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) xx[e] = x[e] * x[e];
+      const T nx = from_next<LPC>(x[0]);
+      const T pxx = from_prev<LPC>(xx[E - 1]);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const T xn = (e + 1 < E) ? x[(e + 1 < E) ? e + 1 : e] : nx;
+        t[e] = xn - xx[e];
+      }
+      const T tp = x[0] - pxx;
+      T part = (T)0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const T tprev = (e > 0) ? t[(e > 0) ? e - 1 : 0] : tp;
+        // g = x (4b t - 2) + 2a - 2b t_prev as three fused multiply-adds
+        g[e] = gfma(nb2m[e], tprev, gfma(x[e], gfma(b4m[e], t[e], nc2m[e]), cam[e]));
+        if (LOGP) {
+          const T am = a - x[e];
+          const T s = keep(b * (t[e] * t[e]) + am * am, ms[e]);
+          part = (e == 0) ? s : part + s;
+        }
+      }
+      return part;
+    }
+  }
+  // The 64-lane form (eval64) for a chain spread over a workgroup: the wave-
   // boundary neighbours come from LDS instead of reading 0 (same operands,
   // same bits as a single group holding the whole chain). The [.] factors
   // are the constants themselves in waves without a chain-end coordinate

@@ -50,16 +50,18 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
 #pragma unroll
       for (int k = 0; k < S; ++k) zs[e][k] = (i < D) ? zs[e][k] : (T)0;
     }
+    T kp[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) {
-      T kp = (T)0;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const T sq = zs[e][k] * zs[e][k];
-        kp = (e == 0) ? sq : kp + sq;
+        kp[k] = (e == 0) ? sq : kp[k] + sq;
       }
-      kes[k] = group_sum<LPC>(kp) * (T)0.5;  // 2. kinetic energy
     }
+    group_sum_n<LPC>(kp);  // 2. kinetic energies, the S sums interleaved
+#pragma unroll
+    for (int k = 0; k < S; ++k) kes[k] = kp[k] * (T)0.5;
     T us[S];
     uniforms_of(draw_block(a.seed, ucid, blk, TAG_ACC, 0u), us);
     if constexpr (LPC == 64) {
@@ -146,23 +148,49 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
     if (a.lf_unroll == 4)
       for (; l + 4 < a.L; l += 4) { lf(); lf(); lf(); lf(); }
     for (; l + 1 < a.L; ++l) lf();
+    // 6. proposed kinetic energy, from the in-lane sums of p'^2
+    auto kin_part = [&]() __attribute__((always_inline)) {
+      T kq = (T)0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const T sq = p1[e] * p1[e];
+        kq = (e == 0) ? sq : kq + sq;
+      }
+      return kq;
+    };
+    T ke1;
     if (a.L >= 1) {
 #pragma unroll
       for (int e = 0; e < E; ++e) p1[e] = p1[e] + gh[e];
 #pragma unroll
       for (int e = 0; e < E; ++e) q1[e] = q1[e] + p1[e] * eps;
-      lp1 = tg.template eval<LPC, E, true>(q1, g1, lane);
+      using TL = typename Bare<decltype(tg)>::type;  // the per-lane target view
+      if constexpr (requires { TL::template has_part<LPC>; }) {
+        if constexpr (TL::template has_part<LPC>) {
+          // the log-density and kinetic-energy sums reduced together
+          T sums[2];
+          sums[0] = tg.template eval_part<LPC, E>(q1, g1, lane);
 #pragma unroll
-      for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
-    }
-    // 6. proposed kinetic energy
-    T kq = (T)0;
+          for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+          sums[1] = kin_part();
+          group_sum_n<LPC>(sums);
+          lp1 = tg.finish(sums[0]);
+          ke1 = sums[1] * (T)0.5;
+        } else {
+          lp1 = tg.template eval<LPC, E, true>(q1, g1, lane);
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const T sq = p1[e] * p1[e];
-      kq = (e == 0) ? sq : kq + sq;
+          for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+          ke1 = group_sum<LPC>(kin_part()) * (T)0.5;
+        }
+      } else {
+        lp1 = tg.template eval<LPC, E, true>(q1, g1, lane);
+#pragma unroll
+        for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+        ke1 = group_sum<LPC>(kin_part()) * (T)0.5;
+      }
+    } else {
+      ke1 = group_sum<LPC>(kin_part()) * (T)0.5;
     }
-    const T ke1 = group_sum<LPC>(kq) * (T)0.5;
     // 7-9. Metropolis accept (NaN log_alpha rejects)
     const T log_alpha = (lp1 - lp) + (ke0 - ke1);
     if (log_alpha >= lnu) {
