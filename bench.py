@@ -132,6 +132,7 @@ def main():
         "note": "SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) / (1024 SIMDs x kernel cycles)"}
 
     copy_gbs = copy_ceiling(lib) if rank == 0 else None
+    ns = north_star_check(gm, a, dtype) if rank == 0 and world == 1 else None
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
@@ -155,10 +156,10 @@ def main():
                                    f"eps={a.eps}, n_leapfrog={L}, all {a.steps} transitions collected",
                        "chains_per_gpu": C_loc, "dim": D, "n_leapfrog": L, "step_size": a.eps,
                        "layout": f"{lanes}x{elems}", "parallelism": f"chains sharded x{world}"},
-            "ess_per_sec": float(np.mean(ess)) / t_max,
-            "ess_min_per_sec": float(np.min(ess)) / t_max,
-            "ess": {"min": float(np.min(ess)), "mean": float(np.mean(ess))},
-            "rhat": {"min": float(np.min(rhat)), "max": float(np.max(rhat))},
+            "ess_per_sec": fin(np.mean(ess) / t_max),
+            "ess_min_per_sec": fin(np.min(ess) / t_max),
+            "ess": {"min": fin(np.min(ess)), "mean": fin(np.mean(ess))},
+            "rhat": {"min": fin(np.min(rhat)), "max": fin(np.max(rhat))},
             "diag_seconds": t_diag,
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
@@ -170,12 +171,42 @@ def main():
                                   "issue": valu_issue},
                          "copy_ceiling_gbs": copy_gbs},
             "cpu_baseline": cpu,
+            "north_star_check": ns,
         }
         print(json.dumps(line), flush=True)
     if comm is not None:
         comm.close()
     sampler.close()
     cp.close()
+
+
+def north_star_check(gm, a, dtype, chains=16384):
+    """BASELINE.json north_star's target shape: >= 10^4 chains of 64-D
+    Rosenbrock HMC on one GPU (same eps, L and collection as the bench; device
+    time of one launch). Reported beside the headline, never as `value`."""
+    D, L, n = a.dim, a.leapfrog, 100
+    s = gm.HMC(gm.RosenbrockND(), gm.init_with_seed(chains, D, 43, np.float64).astype(dtype),
+               a.eps, L, dtype=dtype).set_seed(43)
+    try:
+        s.reserve(n)
+        s.run_positions(0, 20)
+        s.run_positions(n, 0)
+        ms, launches = s.last_run_stats()
+    finally:
+        s.close()
+    sb = np.dtype(dtype).itemsize
+    b_step = (L * (6 * D + 1) + (4 * D + 2) + D) * sb
+    gbs = b_step * chains * n / (ms * 1e-3) / 1e9
+    return {"chains": chains, "chain_leapfrogs_per_s": chains * L * n / (ms * 1e-3),
+            "launch_ms": ms / max(launches, 1), "hbm_equiv_gbs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS,
+            "target": ">= 1e4 chains at >= 50% of the HBM-read roofline (BASELINE.json north_star)"}
+
+
+def fin(v):
+    """float, or None where undefined (diagnostics need >= 4 draws): keeps the
+    JSON line strict."""
+    v = float(v)
+    return v if np.isfinite(v) else None
 
 
 def copy_ceiling(lib, nbytes=1 << 30, reps=5):
