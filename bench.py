@@ -133,6 +133,7 @@ def main():
 
     copy_gbs = copy_ceiling(lib) if rank == 0 else None
     ns = north_star_check(gm, a, dtype) if rank == 0 and world == 1 else None
+    host_out = host_output_rate(lib, sampler, a) if rank == 0 and world == 1 else None
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
@@ -172,12 +173,28 @@ def main():
                          "copy_ceiling_gbs": copy_gbs},
             "cpu_baseline": cpu,
             "north_star_check": ns,
+            "host_output": host_out,
         }
         print(json.dumps(line), flush=True)
     if comm is not None:
         comm.close()
     sampler.close()
     cp.close()
+
+
+def host_output_rate(lib, sampler, a):
+    """The same transitions through gm_run (HMC::run, hmc.rs:164-181): the
+    [C, N, D] sample returned in a host array (device transpose + D2H into
+    pageable memory). The PCIe-inclusive rate; never `value`."""
+    from general_mcmc_amd import _lib
+    sampler.run(a.steps, 0)  # warm (host array, staging buffers)
+    _lib.check(lib.gm_device_synchronize())
+    t0 = time.perf_counter()
+    out = sampler.run(a.steps, 0)
+    t = time.perf_counter() - t0
+    C, N, D = out.shape
+    return {"chain_leapfrogs_per_s": C * a.leapfrog * N / t, "seconds": t,
+            "sample_bytes": int(out.nbytes), "d2h_gbs_incl_sampling": out.nbytes / t / 1e9}
 
 
 def north_star_check(gm, a, dtype, chains=16384):
