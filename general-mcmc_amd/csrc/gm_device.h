@@ -473,8 +473,22 @@ template <class T, int LPC, int E> struct GaussLane {
   int D;
   const T* sprec;  // LDS [D][S] or null
   T* sd;           // LDS slot of this lane group's d [S]
+  // unreduced log-density term for callers that reduce it together with
+  // another per-chain sum: logp = finish(group_sum(eval_part(...)))
+  template <int LPC_> static constexpr bool has_part = true;
+  template <int LPC_, int E_>
+  __device__ __forceinline__ T eval_part(const T (&x)[E], T (&g)[E], int lane) const {
+    return eval_impl<LPC_, E_, true>(x, g, lane);
+  }
+  __device__ __forceinline__ T finish(T total) const { return nc - total * (T)0.5; }
   template <int LPC_, int E_, bool LOGP>
   __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int lane) const {
+    const T part = eval_impl<LPC_, E_, LOGP>(x, g, lane);
+    if (LOGP) return finish(group_sum<LPC>(part));
+    return (T)0;
+  }
+  template <int LPC_, int E_, bool LOGP>
+  __device__ __forceinline__ T eval_impl(const T (&x)[E], T (&g)[E], int lane) const {
     static_assert(LPC_ == LPC && E_ == E, "layout mismatch");
     T d[E], w[E];
 #pragma unroll
@@ -545,8 +559,7 @@ template <class T, int LPC, int E> struct GaussLane {
         part = (e == 0) ? s : part + s;
       }
     }
-    if (LOGP) return nc - group_sum<LPC>(part) * (T)0.5;
-    return (T)0;
+    return part;
   }
 };
 

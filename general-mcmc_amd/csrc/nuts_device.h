@@ -117,9 +117,17 @@ __device__ __forceinline__ bool no_uturn(const T (&qm)[E], const T (&qp)[E], con
   T d[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) d[e] = qp[e] - qm[e];
-  const T dm = dot_group<LPC, E>(d, pm);
-  const T dp = dot_group<LPC, E>(d, pp);
-  return dm >= (T)0 && dp >= (T)0;
+  // dot_group(d, pm), dot_group(d, pp), their reductions interleaved
+  T dd[2];
+  dd[0] = d[0] * pm[0];
+  dd[1] = d[0] * pp[0];
+#pragma unroll
+  for (int e = 1; e < E; ++e) {
+    dd[0] = dd[0] + d[e] * pm[e];
+    dd[1] = dd[1] + d[e] * pp[e];
+  }
+  group_sum_n<LPC>(dd);
+  return dd[0] >= (T)0 && dd[1] >= (T)0;
 }
 
 // MassMatrix::kinetic (:226-253), canonical-order sum of the per-coordinate
@@ -158,6 +166,41 @@ __device__ __forceinline__ T leapfrog_m(const TG& tg, const MassDev<T, E>& M, T 
 #pragma unroll
   for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
   return lp;
+}
+
+// leapfrog_m followed by kinetic_m at the new point. With the identity
+// metric and a target that exposes its unreduced log-density term
+// (eval_part / finish), both per-chain sums are reduced together: the same
+// stages and bits as the two separate reductions.
+template <int LPC, int E, class T, class TG>
+__device__ __forceinline__ void leaf_leapfrog(const TG& tg, const MassDev<T, E>& M, T (&q)[E], T (&p)[E],
+                                              T (&g)[E], T epsv, int lane, T& lp, T& kin) {
+  using TL = typename Bare<TG>::type;
+  if constexpr (requires { TL::template has_part<LPC>; }) {
+    if constexpr (TL::template has_part<LPC>) {
+      if (M.kind == 0) {
+        const T h = epsv * (T)0.5;
+#pragma unroll
+        for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
+#pragma unroll
+        for (int e = 0; e < E; ++e) q[e] = q[e] + p[e] * epsv;
+        T sums[2];
+        sums[0] = tg.template eval_part<LPC, E>(q, g, lane);
+#pragma unroll
+        for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
+        T kp = p[0] * p[0];
+#pragma unroll
+        for (int e = 1; e < E; ++e) kp = kp + p[e] * p[e];
+        sums[1] = kp;
+        group_sum_n<LPC>(sums);
+        lp = tg.finish(sums[0]);
+        kin = (T)0.5 * sums[1];
+        return;
+      }
+    }
+  }
+  lp = leapfrog_m<LPC, E>(tg, M, q, p, g, epsv, lane);
+  kin = kinetic_m<LPC, E>(M, p, lane);
 }
 
 // stop_criterion_with_mass (:1354-1378), the top-level U-turn
@@ -442,9 +485,10 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       long long tna = 0;
       const long long nleaves = 1LL << j;
       for (long long l = 0; l < nleaves; ++l) {
-        const T lp = leapfrog_m<LPC, E>(tg, M, qe, pe, ge, epsv, lane);
+        T lp, kin;
+        leaf_leapfrog<LPC, E>(tg, M, qe, pe, ge, epsv, lane, lp, kin);
         ++nlf;
-        const T joint = lp - kinetic_m<LPC, E>(M, pe, lane);
+        const T joint = lp - kin;
         tn = (logu < joint) ? 1 : 0;
         ts = (logu - (T)1000) < joint;
         ta = rust_min1(gexp(joint - joint0));
