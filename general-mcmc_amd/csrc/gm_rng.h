@@ -350,6 +350,42 @@ GM_HD u32x4 draw_block(uint64_t seed, uint32_t chain, uint64_t blk, uint32_t tag
   return philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
+#if defined(__HIPCC__)
+// Philox round keys held in VGPRs (device only): a VALU operation with an
+// SGPR source issues at about half rate on gfx950 at 4 waves per SIMD
+// (tools/probes/bank_probe.hip), and the vector Philox of the HMC draw block
+// XORs a key into every round. Same values as philox(c, k0, k1).
+struct PhiloxKeys {
+  uint32_t k0[10], k1[10];
+};
+__device__ __forceinline__ PhiloxKeys philox_keys(uint64_t seed) {
+  PhiloxKeys K;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t a = k0, b = k1;
+    asm volatile("" : "+v"(a), "+v"(b));
+    K.k0[r] = a;
+    K.k1[r] = b;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return K;
+}
+__device__ __forceinline__ u32x4 draw_block_k(const PhiloxKeys& K, uint32_t chain, uint64_t blk, uint32_t tag,
+                                              uint32_t idx) {
+  u32x4 c{idx, chain, (uint32_t)blk, tag | ((uint32_t)(blk >> 32) << 8)};
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
+    c = u32x4{hi1 ^ c.y ^ K.k0[r], lo1, hi0 ^ c.w ^ K.k1[r], lo0};
+  }
+  return c;
+}
+#endif
+
 // the S normals of a block
 GM_HD void normals_of(u32x4 x, float (&z)[4]) {
   float c, s;

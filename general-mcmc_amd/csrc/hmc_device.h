@@ -32,6 +32,7 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
   T lp = tg.template eval<LPC, E, true>(q, g, lane);
   long long acc = 0;
   constexpr int S = Blk<T>::S;  // one Philox block serves S transitions
+  const PhiloxKeys pk = philox_keys(a.seed);  // momentum streams' round keys, in VGPRs
   // Draw blocks: A = the current block (front = this step), B = the next
   // one, prefetched. Each wave prefetches on the step whose index matches its
   // wave phase, so the waves of a SIMD are not all in the Philox/Box-Muller
@@ -46,7 +47,7 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
-      normals_of(draw_block(a.seed, cid, blk, TAG_MOM, (uint32_t)i), zs[e]);
+      normals_of(draw_block_k(pk, cid, blk, TAG_MOM, (uint32_t)i), zs[e]);
 #pragma unroll
       for (int k = 0; k < S; ++k) zs[e][k] = (i < D) ? zs[e][k] : (T)0;
     }
