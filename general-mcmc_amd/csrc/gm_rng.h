@@ -350,7 +350,7 @@ GM_HD u32x4 draw_block(uint64_t seed, uint32_t chain, uint64_t blk, uint32_t tag
   return philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
-#if defined(__HIPCC__)
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
 // Philox round keys held in VGPRs (device only): a VALU operation with an
 // SGPR source issues at about half rate on gfx950 at 4 waves per SIMD
 // (tools/probes/bank_probe.hip), and the vector Philox of the HMC draw block
@@ -372,8 +372,8 @@ __device__ __forceinline__ PhiloxKeys philox_keys(uint64_t seed) {
   }
   return K;
 }
-__device__ __forceinline__ u32x4 draw_block_k(const PhiloxKeys& K, uint32_t chain, uint64_t blk, uint32_t tag,
-                                              uint32_t idx) {
+__device__ __forceinline__ u32x4 draw_block(const PhiloxKeys& K, uint32_t chain, uint64_t blk, uint32_t tag,
+                                            uint32_t idx) {
   u32x4 c{idx, chain, (uint32_t)blk, tag | ((uint32_t)(blk >> 32) << 8)};
 #pragma unroll
   for (int r = 0; r < 10; ++r) {

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
-      normals_of(draw_block_k(pk, cid, blk, TAG_MOM, (uint32_t)i), zs[e]);
+      normals_of(draw_block(pk, cid, blk, TAG_MOM, (uint32_t)i), zs[e]);
 #pragma unroll
       for (int k = 0; k < S; ++k) zs[e][k] = (i < D) ? zs[e][k] : (T)0;
     }
