@@ -154,3 +154,25 @@ def test_bad_arguments_raise(gm):
         gm.HMC(gm.RosenbrockND(), gm.init_det(2, 16385, np.float32), 0.1, 2)
     with pytest.raises(gm.GMError):
         gm.split_rhat_mean_ess(np.zeros((2, 1, 3)))
+
+
+def test_reserve_and_host_output_match_device_samples(gm):
+    """gm_sampler_reserve pre-sizes the sample buffer (no allocation inside the
+    bench's timed region) without changing results; gm_run's host [C,N,D]
+    array is the transpose of the device [N,C,D] samples of the same run."""
+    C, D, L = 128, 64, 10
+    x0 = gm.init_with_seed(C, D, 5, np.float32)
+    a = gm.HMC(gm.RosenbrockND(), x0, 0.01, L).set_seed(9)
+    b = gm.HMC(gm.RosenbrockND(), x0, 0.01, L).set_seed(9)
+    b.reserve(40)
+    b.reserve(3)  # grow-only: a smaller request keeps the buffer
+    da = a.run_positions(6, 2).to_host()
+    db = b.run_positions(6, 2).to_host()
+    np.testing.assert_array_equal(da, db)
+    ha = a.run(5, 0)
+    ds = b.run_positions(5, 0)
+    np.testing.assert_array_equal(ha, ds.to_host())
+    rows = ds.block(0, 5, 0, C)  # the device layout, [N, C, D]
+    np.testing.assert_array_equal(ha, np.ascontiguousarray(rows.transpose(1, 0, 2)))
+    with pytest.raises(gm.GMError):
+        b.reserve(-1)
