@@ -137,6 +137,7 @@ def main():
     copy_gbs = copy_ceiling(lib) if rank == 0 else None
     ns = north_star_check(gm, a, dtype) if rank == 0 and world == 1 and a.north_star else None
     host_out = host_output_rate(lib, sampler, a) if rank == 0 and world == 1 else None
+    per_lf = per_leapfrog_hbm(a, dtype) if rank == 0 and world == 1 else None
 
     cpu = None
     if rank == 0 and world == 1 and a.cpu_seconds > 0:
@@ -173,7 +174,8 @@ def main():
                                   "peak_tflops": VALU_F32_PEAK_TFLOPS,
                                   "frac": achieved_tflops / VALU_F32_PEAK_TFLOPS,
                                   "issue": valu_issue},
-                         "copy_ceiling_gbs": copy_gbs},
+                         "copy_ceiling_gbs": copy_gbs,
+                         "per_leapfrog_hbm": per_lf},
             "cpu_baseline": cpu,
             "north_star_check": ns,
             "host_output": host_out,
@@ -183,6 +185,22 @@ def main():
         comm.close()
     sampler.close()
     cp.close()
+
+
+def per_leapfrog_hbm(a, dtype, chains=1 << 20, reps=20):
+    """The unfused, per-leapfrog design the HBM roofline is written for
+    (SURVEY.md §8(d)): gm_bv_leapfrog, one kernel per leapfrog with q, p, g
+    and logp in HBM, at an HBM-resident size (2^20 chains: 256 MiB per
+    array); achieved = B_alg (6D+1)*s per chain-leapfrog x chains / time."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        from hbm_leapfrog import measure
+        r = measure(chains, a.dim, dtype, reps)
+    except Exception as e:  # reported, never fatal to the bench line
+        return {"error": str(e)}
+    return {"kernel": "leapfrog_hbm_kernel", "chains": chains, "achieved": r["achieved_gbs"],
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": r["hbm_frac"], "us_per_leapfrog": r["us_per_leapfrog"],
+            "chain_leapfrogs_per_s": r["chain_leapfrogs_per_s"]}
 
 
 def host_output_rate(lib, sampler, a):

@@ -128,6 +128,7 @@ SIGNATURES = {
     "gm_bv_target_create": (_ip, [C.POINTER(gm_target), _ip, C.POINTER(_vp)]),
     "gm_bv_logp_and_grad": (_ip, [_vp, _i64, _vp, _vp, _vp]),
     "gm_bv_target_destroy": (_ip, [_vp]),
+    "gm_bv_leapfrog": (_ip, [_vp, _i64, _vp, _vp, _vp, _vp, C.c_double]),
 }
 
 _lib = None

@@ -181,6 +181,15 @@ class BatchTarget:
         _lib.check(self.lib.gm_bv_logp_and_grad(self.h, x.n_chains, _vp(x), _vp(grad), _vp(logp)))
         return logp
 
+    def leapfrog(self, q: DeviceMatrix, p: DeviceMatrix, grad: DeviceMatrix, logp: DeviceMatrix | None,
+                 step_size) -> None:
+        """One leapfrog in place, state in device memory (gm_bv_leapfrog: the
+        loop body of batched_hmc.rs:166-190 as one kernel)."""
+        _same(q, p)
+        _same(q, grad)
+        _lib.check(self.lib.gm_bv_leapfrog(self.h, q.n_chains, _vp(q), _vp(p), _vp(grad),
+                                           _vp(logp), float(step_size)))
+
     def close(self):
         if getattr(self, "h", None) is not None:
             self.lib.gm_bv_target_destroy(self.h)
@@ -199,7 +208,7 @@ class BatchedGenericHMC:
     (batched_hmc.rs:129-163) with the leapfrog of 166-190."""
 
     def __init__(self, target, initial_positions, step_size: float, n_leapfrog: int, seed: int = 0,
-                 chain_offset: int = 0):
+                 chain_offset: int = 0, fused_leapfrog: bool = False):
         x0 = np.ascontiguousarray(initial_positions)
         self.dtype = x0.dtype
         self.n_chains, self.dim = x0.shape
@@ -214,6 +223,8 @@ class BatchedGenericHMC:
         self.seed = int(seed)
         self.chain_offset = int(chain_offset)
         self.t = 0  # transition index (keys the random streams)
+        # one gm_bv_leapfrog kernel per leapfrog instead of four ops (same bits)
+        self.fused_leapfrog = bool(fused_leapfrog)
 
     def set_seed(self, seed: int) -> "BatchedGenericHMC":
         self.seed, self.t = int(seed), 0
@@ -222,6 +233,10 @@ class BatchedGenericHMC:
     def _leapfrog(self) -> DeviceMatrix:
         half = self.dtype.type(0.5) * self.step_size
         logp = self.target.logp_and_grad(self.proposal_pos, self.grad)
+        if self.fused_leapfrog:
+            for _ in range(self.n_leapfrog):
+                self.target.leapfrog(self.proposal_pos, self.proposal_mom, self.grad, logp, self.step_size)
+            return logp
         for _ in range(self.n_leapfrog):
             add_scaled_assign(self.proposal_mom, self.grad, half)
             add_scaled_assign(self.proposal_pos, self.proposal_mom, self.step_size)

@@ -60,6 +60,9 @@ hipError_t launch_mh(gm_dtype dt, const TargetDev& tg, const Layout& lay, const 
                      hipStream_t st);
 
 // ---- target evaluation -----------------------------------------------------
+// one leapfrog of n chains, state in HBM (util_device.h leapfrog_hbm_kernel)
+hipError_t launch_leapfrog_hbm(gm_dtype dt, const TargetDev& tg, const Layout& lay, long long n, void* q,
+                               void* p, void* g, void* logp, double eps, hipStream_t st);
 hipError_t launch_logp_grad(gm_dtype dt, const TargetDev& tg, const Layout& lay, long long n,
                             const void* x, void* logp, void* grad, hipStream_t st);
 

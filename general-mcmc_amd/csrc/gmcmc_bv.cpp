@@ -148,6 +148,17 @@ int gm_bv_logp_and_grad(gm_bv_target* t, int64_t C, const void* x, void* grad, v
   const Layout lay = default_layout(t->tg.D, t->dt, t->tg.kind);
   return bv_status(launch_logp_grad(t->dt, t->tg, lay, C, x, logp, grad, nullptr), "logp_and_grad");
 }
+int gm_bv_leapfrog(gm_bv_target* t, int64_t C, void* q, void* p, void* g, void* logp, double step_size) {
+  BV_REQ(t != nullptr, "target is NULL");
+  BV_REQ(C >= 0, "bad size");
+  BV_REQ(t->tg.kind != GM_TARGET_CUSTOM,
+         "gm_bv_leapfrog: built-in targets only (compose gm_bv_add_scaled_assign and gm_bv_logp_and_grad)");
+  if (C == 0) return GM_OK;
+  BV_REQ(q && p && g, "NULL pointer");
+  const Layout lay = default_layout(t->tg.D, t->dt, t->tg.kind);
+  BV_REQ(!layout_is_wide(lay), "gm_bv_leapfrog: dim <= 1024");
+  return bv_status(launch_leapfrog_hbm(t->dt, t->tg, lay, C, q, p, g, logp, step_size, nullptr), "leapfrog");
+}
 int gm_bv_target_destroy(gm_bv_target* t) {
   if (!t) return GM_OK;
   if (t->d_mu) hipFree(t->d_mu);

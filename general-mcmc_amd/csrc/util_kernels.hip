@@ -64,6 +64,19 @@ hipError_t launch_logp_grad(gm_dtype dt, const TargetDev& tg, const Layout& lay,
   });
 }
 
+hipError_t launch_leapfrog_hbm(gm_dtype dt, const TargetDev& tg, const Layout& lay, long long n, void* q,
+                               void* p, void* g, void* logp, double eps, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  return dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
+    const long long threads = n * LPC;
+    const unsigned blocks = (unsigned)((threads + 255) / 256);
+    const size_t lds = t.template lds_bytes<LPC, E>();
+    hipLaunchKernelGGL((leapfrog_hbm_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), lds, st, n, tg.D,
+                       (T*)q, (T*)p, (T*)g, (T*)logp, (T)eps, t);
+    return hipGetLastError();
+  });
+}
+
 template <class T>
 __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ src, T* __restrict__ dst,
                                                         long long rows, long long C, long long D) {

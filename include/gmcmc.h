@@ -370,6 +370,14 @@ int gm_bv_target_create(const gm_target* target, gm_dtype dtype, gm_bv_target** 
 /* grad[c,:] = d logp / d x at x[c,:]; returns logp[c] (either output may be NULL) */
 int gm_bv_logp_and_grad(gm_bv_target* t, int64_t n_chains, const void* x, void* grad, void* logp);
 int gm_bv_target_destroy(gm_bv_target* t);
+/* One leapfrog of n_chains chains with q, p, g ([C][D]) and logp ([C],
+ * nullable) in device memory, updated in place: the loop body of
+ * BatchedGenericHMC::leapfrog (batched_hmc.rs:166-190) -- add_scaled_assign
+ * (euclidean.rs:392-394) of the half kick, the drift, logp_and_grad
+ * (hmc.rs:42-61), the second half kick -- as one kernel. Bitwise the composed
+ * ops. Built-in targets, dim <= 1024. */
+int gm_bv_leapfrog(gm_bv_target* t, int64_t n_chains, void* q, void* p, void* g, void* logp,
+                   double step_size);
 
 #ifdef __cplusplus
 }

@@ -111,6 +111,20 @@ def test_composed_step_equals_fused_kernel(gm, bv, name, mk, D, dtype, eps, L):
     np.testing.assert_array_equal(composed.positions(), fused.positions())
 
 
+@pytest.mark.parametrize("name,mk,D,dtype,eps,L", CASES, ids=[c[0] for c in CASES])
+def test_hbm_leapfrog_equals_composed_ops(gm, bv, name, mk, D, dtype, eps, L):
+    """gm_bv_leapfrog (one kernel per leapfrog, state in HBM) == the four
+    composed ops == the fused kernel, bitwise."""
+    C, off = 48, 1000
+    x0 = gm.init_with_seed(C, D, 11, dtype)
+    composed = bv.BatchedGenericHMC(mk(gm), x0, eps, L, seed=9, chain_offset=off)
+    per_lf = bv.BatchedGenericHMC(mk(gm), x0, eps, L, seed=9, chain_offset=off, fused_leapfrog=True)
+    fused = gm.HMC(mk(gm), x0, eps, L, dtype=dtype, chain_offset=off).set_seed(9)
+    a, b, c = composed.run(3, 1), per_lf.run(3, 1), fused.run(3, 1)
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(b, c)
+
+
 def test_bv_rejects_bad_arguments(gm, bv):
     a = bv.DeviceMatrix((4, 3), np.float32)
     b = bv.DeviceMatrix((4, 2), np.float32)
