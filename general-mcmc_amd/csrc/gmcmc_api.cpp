@@ -9,6 +9,7 @@
 // inside one launch with the chain state resident in registers.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -18,6 +19,7 @@
 #include <random>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gm_jit.h"
@@ -144,6 +146,8 @@ struct gm_sampler {
   size_t samples_bytes = 0;
   void* d_tmp = nullptr;
   size_t tmp_bytes = 0;
+  void* h_stage[2] = {nullptr, nullptr};  // pinned D2H staging slots (gm_copy_samples)
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
   void* d_zs = nullptr;  // wide-layout HMC momentum scratch
   size_t zs_bytes = 0;
   Layout lay;
@@ -736,6 +740,61 @@ int gm_run_device_progress(gm_sampler* s, int64_t n_collect, int64_t n_discard,
   return GM_OK;
 }
 
+// Device -> caller's (pageable) host memory through two pinned staging slots:
+// the DMA of chunk i runs while host threads copy chunk i-1 out of the other
+// slot. The threads also take the first-touch page faults of a fresh output
+// array in parallel, which a single-threaded pageable hipMemcpy serialises.
+static constexpr size_t kStageChunk = (size_t)16 << 20;
+
+static int host_copy_threads() {
+  const char* e = std::getenv("OMP_NUM_THREADS");
+  int n = e ? std::atoi(e) : (int)std::thread::hardware_concurrency();
+  return n < 1 ? 1 : (n > 16 ? 16 : n);
+}
+
+static void parallel_memcpy(char* dst, const char* src, size_t n, int threads) {
+  const size_t min_part = (size_t)1 << 20;
+  int t = (int)std::min<size_t>((size_t)threads, (n + min_part - 1) / min_part);
+  if (t <= 1) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  const size_t part = (n + t - 1) / t;
+  for (int i = 1; i < t; ++i) {
+    const size_t o = (size_t)i * part;
+    if (o >= n) break;
+    pool.emplace_back([=] { std::memcpy(dst + o, src + o, std::min(part, n - o)); });
+  }
+  std::memcpy(dst, src, std::min(part, n));
+  for (auto& th : pool) th.join();
+}
+
+static int stage_to_host(gm_sampler* s, void* out, const void* dsrc, size_t bytes) {
+  if (bytes == 0) return GM_OK;
+  if (!s->h_stage[0]) {
+    for (int k = 0; k < 2; ++k) {
+      GM_HIP(hipHostMalloc(&s->h_stage[k], kStageChunk, hipHostMallocDefault));
+      GM_HIP(hipEventCreateWithFlags(&s->stage_ev[k], hipEventDisableTiming));
+    }
+  }
+  const int threads = host_copy_threads();
+  const size_t n_chunks = (bytes + kStageChunk - 1) / kStageChunk;
+  for (size_t i = 0; i <= n_chunks; ++i) {
+    if (i < n_chunks) {  // DMA of chunk i into slot i % 2
+      const size_t o = i * kStageChunk, n = std::min(kStageChunk, bytes - o);
+      GM_HIP(hipMemcpyAsync(s->h_stage[i & 1], (const char*)dsrc + o, n, hipMemcpyDeviceToHost, s->stream));
+      GM_HIP(hipEventRecord(s->stage_ev[i & 1], s->stream));
+    }
+    if (i >= 1) {  // host copy of chunk i-1 while chunk i is in flight
+      const size_t j = i - 1, o = j * kStageChunk, n = std::min(kStageChunk, bytes - o);
+      GM_HIP(hipEventSynchronize(s->stage_ev[j & 1]));
+      parallel_memcpy((char*)out + o, (const char*)s->h_stage[j & 1], n, threads);
+    }
+  }
+  return GM_OK;
+}
+
 int gm_copy_samples(gm_sampler* s, void* out) {
   GM_REQ(s && out, "bad arguments");
   GM_HIP(hipSetDevice(s->device));
@@ -750,9 +809,7 @@ int gm_copy_samples(gm_sampler* s, void* out) {
     set_error(std::string("transpose failed: ") + hipGetErrorString(e));
     return GM_EHIP;
   }
-  GM_HIP(hipMemcpyAsync(out, s->d_tmp, bytes, hipMemcpyDeviceToHost, s->stream));
-  GM_HIP(hipStreamSynchronize(s->stream));
-  return GM_OK;
+  return stage_to_host(s, out, s->d_tmp, bytes);
 }
 
 int gm_copy_sample_block(gm_sampler* s, int64_t row0, int64_t n_rows, int64_t chain0, int64_t n_chains,
@@ -1202,6 +1259,10 @@ int gm_destroy(gm_sampler* s) {
   if (s->d_acc) hipFree(s->d_acc);
   if (s->d_samples) hipFree(s->d_samples);
   if (s->d_tmp) hipFree(s->d_tmp);
+  for (int k = 0; k < 2; ++k) {
+    if (s->h_stage[k]) hipHostFree(s->h_stage[k]);
+    if (s->stage_ev[k]) hipEventDestroy(s->stage_ev[k]);
+  }
   if (s->d_trk) hipFree(s->d_trk);
   if (s->d_mct) hipFree(s->d_mct);
   nuts_free_state(&s->nuts);

@@ -176,3 +176,19 @@ def test_reserve_and_host_output_match_device_samples(gm):
     np.testing.assert_array_equal(ha, np.ascontiguousarray(rows.transpose(1, 0, 2)))
     with pytest.raises(gm.GMError):
         b.reserve(-1)
+
+
+def test_host_output_multi_chunk_staging(gm):
+    """gm_run's host array goes through two 16 MiB pinned staging slots; a
+    sample of 2.5 chunks plus a ragged tail (41 MB) arrives intact: equal to
+    the device rows of the same run, transposed to [C, N, D]."""
+    C, D, N = 4099, 50, 50  # 4099*50*50*4 B = 41 MB, not a multiple of the chunk
+    x0 = gm.init_with_seed(C, D, 11, np.float32)
+    a = gm.HMC(gm.RosenbrockND(), x0, 0.01, 2).set_seed(3)
+    b = gm.HMC(gm.RosenbrockND(), x0, 0.01, 2).set_seed(3)
+    ha = a.run(N, 1)
+    assert ha.shape == (C, N, D)
+    rows = b.run_positions(N, 1).block(0, N, 0, C)
+    np.testing.assert_array_equal(ha, np.ascontiguousarray(rows.transpose(1, 0, 2)))
+    hb = a.run(1, 0)  # a small copy after a large one (one partial chunk)
+    np.testing.assert_array_equal(hb[:, 0, :], b.run_positions(1, 0).block(0, 1, 0, C)[0])
