@@ -102,6 +102,7 @@ SIGNATURES = {
     "gm_comm_init": (_ip, [_vp, _i32, _i32, C.POINTER(_vp)]),
     "gm_comm_destroy": (_ip, [_vp]),
     "gm_split_rhat_ess_dist": (_ip, [_vp, _vp, _ip, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
+    "gm_split_rhat_ess_shards": (_ip, [_vp, _ip, _ip, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
     # run_progress statistics
     "gm_run_progress_cb": (_ip, [_vp, _i64, _i64, _vp, _vp, _vp, PROGRESS_FN, _vp, _dbl]),
     "gm_sampler_chain_stats": (_ip, [_vp, C.POINTER(_u64), _vp, _vp, _vp]),

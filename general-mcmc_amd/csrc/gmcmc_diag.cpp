@@ -233,4 +233,39 @@ int gm_split_rhat_ess_dist(gm_comm* comm, const void* dev_sample, gm_dtype dtype
                     stride_param, comm, rhat_out, ess_out, comm->stream);
 }
 
+int gm_split_rhat_ess_shards(const void* const* dev_shards, int32_t n_shards, gm_dtype dtype,
+                             int64_t n_chains_per_shard, int64_t n_draws, int64_t n_params,
+                             int64_t stride_chain, int64_t stride_draw, int64_t stride_param,
+                             float* rhat_out, float* ess_out) {
+  // The exchange of gm_split_rhat_ess_dist with every rank's shard on this
+  // device: shard r's per-split-chain summaries are written where the RCCL
+  // all-gather puts rank r's block ([R][P][2C], [R][h][P]), then the same
+  // final kernel reads them.
+  GM_REQ(dtype == GM_F32 || dtype == GM_F64, "bad dtype");
+  GM_REQ(dev_shards && n_shards >= 1, "need n_shards >= 1 shard pointers");
+  const int64_t C = n_chains_per_shard, N = n_draws, P = n_params;
+  GM_REQ(C >= 1 && N >= 2 && P >= 1, "need n_chains >= 1, n_draws >= 2, n_params >= 1");
+  GM_REQ(rhat_out && ess_out, "NULL argument");
+  for (int r = 0; r < n_shards; ++r) GM_REQ(dev_shards[r], "shard pointer is NULL");
+  const int h = (int)(N / 2), R = n_shards;
+  DiagBufs& B = diag_bufs();
+  int rc;
+  if ((rc = B.cm_all.alloc(sizeof(double) * 2 * C * P * R)) ||
+      (rc = B.s2_all.alloc(sizeof(double) * 2 * C * P * R)) ||
+      (rc = B.ac_all.alloc(sizeof(double) * h * P * R)) || (rc = B.out.alloc(sizeof(float) * 2 * P)))
+    return rc;
+  double *cm = (double*)B.cm_all.p, *s2 = (double*)B.s2_all.p, *ac = (double*)B.ac_all.p;
+  for (int r = 0; r < R; ++r) {
+    rc = diag_series(dtype, dev_shards[r], C, N, P, stride_chain, stride_draw, stride_param,
+                     cm + (size_t)r * 2 * C * P, s2 + (size_t)r * 2 * C * P, ac + (size_t)r * h * P,
+                     B.ws, nullptr);
+    if (rc) return rc;
+  }
+  rc = diag_final(cm, s2, ac, 2 * C * R, R, h, P, (float*)B.out.p, (float*)B.out.p + P, nullptr);
+  if (rc) return rc;
+  GM_HIP(hipMemcpy(rhat_out, B.out.p, sizeof(float) * P, hipMemcpyDeviceToHost));
+  GM_HIP(hipMemcpy(ess_out, (float*)B.out.p + P, sizeof(float) * P, hipMemcpyDeviceToHost));
+  return GM_OK;
+}
+
 }  // extern "C"

@@ -99,3 +99,23 @@ class Comm:
         if getattr(self, "h", None) is not None:
             self.lib.gm_comm_destroy(self.h)
             self.h = None
+
+
+def split_rhat_ess_shards(shards) -> tuple[np.ndarray, np.ndarray]:
+    """Diagnostics of the union of several DeviceSamples shards on this GPU
+    (equal chain counts, same n_collect and dim), assembled exactly as the
+    RCCL all-gather of Comm.split_rhat_ess assembles the ranks' blocks
+    (gm_split_rhat_ess_shards)."""
+    lib = _lib.require_gpu()
+    d0 = shards[0]
+    for d in shards:
+        if (d.n_chains, d.n_collect, d.dim, np.dtype(d.dtype)) != (d0.n_chains, d0.n_collect, d0.dim,
+                                                                   np.dtype(d0.dtype)):
+            raise ValueError("shards must have equal chain counts, draws, dims and dtypes")
+    ptrs = (C.c_void_p * len(shards))(*[d.ptr for d in shards])
+    rhat = np.empty(d0.dim, dtype=np.float32)
+    ess = np.empty(d0.dim, dtype=np.float32)
+    _lib.check(lib.gm_split_rhat_ess_shards(
+        ptrs, len(shards), _lib.dtype_code(d0.dtype), d0.n_chains, d0.n_collect, d0.dim,
+        d0.dim, d0.n_chains * d0.dim, 1, _lib.ptr(rhat), _lib.ptr(ess)))
+    return rhat, ess

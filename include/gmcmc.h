@@ -280,6 +280,16 @@ int gm_split_rhat_ess_dist(gm_comm* comm, const void* dev_sample, gm_dtype dtype
                            int64_t n_chains_local, int64_t n_draws, int64_t n_params,
                            int64_t stride_chain, int64_t stride_draw, int64_t stride_param,
                            float* rhat_out, float* ess_out);
+/* The same exchange with all R shards on the calling thread's device
+ * (equal chain counts, same strides): shard r's summaries land where the
+ * all-gather puts rank r's, and one final kernel reads them. Equals
+ * split_rhat_mean_ess (stats.rs:439-450) of the concatenated chains, up to
+ * summation order; one process driving several shards uses it, and it
+ * checks the multi-rank assembly on a single GPU. */
+int gm_split_rhat_ess_shards(const void* const* dev_shards, int32_t n_shards, gm_dtype dtype,
+                             int64_t n_chains_per_shard, int64_t n_draws, int64_t n_params,
+                             int64_t stride_chain, int64_t stride_draw, int64_t stride_param,
+                             float* rhat_out, float* ess_out);
 
 /* ---- run_progress with live statistics -------------------------------
  * The reference's run_progress draws progress bars fed by chain trackers:
