@@ -169,6 +169,11 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "hmc_kernel", "launch_ms": launch_ms,
+                         "note": "achieved = SURVEY 8(d) algorithmic bytes (q, p, g round-trip HBM every "
+                                 "leapfrog) / launch time; the fused kernel keeps the state in VGPRs "
+                                 "(traffic = the PMC bytes it moves, mostly the collected samples), so "
+                                 "frac > 1; its real bound is VALU issue (valu); the HBM-bound "
+                                 "per-leapfrog formulation is per_leapfrog_hbm",
                          "algorithmic_bytes_per_launch": bytes_per_launch,
                          "valu": {"achieved_tflops": achieved_tflops,
                                   "peak_tflops": VALU_F32_PEAK_TFLOPS,
