@@ -426,6 +426,9 @@ extern __shared__ __attribute__((aligned(16))) unsigned char gm_dyn_lds[];
 
 // fused multiply-add, one rounding (the oracle's FMA)
 
+#ifndef GM_GEMV_UNROLL
+#define GM_GEMV_UNROLL 4  // columns of the LDS GEMV loop in flight per iteration
+#endif
 template <class T, int LPC, int E> struct GaussLane;
 template <class T> struct GaussT {
   const T* mu;    // [D] device
@@ -512,7 +515,7 @@ template <class T, int LPC, int E> struct GaussLane {
 #pragma unroll
         for (int e = 0; e < E; ++e) w[e] = gfma(pr[e], d0, (T)0);
       }
-#pragma unroll 4
+#pragma unroll GM_GEMV_UNROLL
       for (int j = 1; j < D; ++j) {
         const T dj = sd[j];
 #pragma unroll
