@@ -78,7 +78,7 @@ SIGNATURES = {
     "gm_run_device": (_ip, [_vp, _i64, _i64, C.POINTER(_vp)]),
     "gm_run_device_progress": (_ip, [_vp, _i64, _i64, C.POINTER(_vp)]),
     "gm_run_progress": (_ip, [_vp, _i64, _i64, _vp, _vp, _vp]),
-    "gm_copy_samples": (_ip, [_vp, _vp]),
+    "gm_copy_samples": (_ip, [_vp, _i64, _vp]),
     "gm_copy_sample_block": (_ip, [_vp, _i64, _i64, _i64, _i64, _vp]),
     "gm_get_positions": (_ip, [_vp, _vp]),
     "gm_set_positions": (_ip, [_vp, _vp]),

@@ -21,19 +21,30 @@ class DeviceSamples:
     dim: int
     dtype: type
     owner: "Sampler"
+    generation: int = -1
+
+    def _check_live(self):
+        # the device buffer belongs to the sampler's LAST run: a later run may
+        # have resized (freed) it or overwritten it
+        if self.owner._h is None or self.generation != self.owner._gen:
+            raise RuntimeError("DeviceSamples are stale: the sampler has run again (or was closed) "
+                               "since they were produced")
 
     def to_host(self) -> np.ndarray:
+        self._check_live()
         return self.owner.copy_samples(self.n_collect)
 
     def block(self, row0: int, n_rows: int, chain0: int, n_chains: int) -> np.ndarray:
         """Rows [row0, row0+n_rows) x chains [chain0, chain0+n_chains) on the
         host, [n_rows, n_chains, dim] (one strided device-to-host copy)."""
+        self._check_live()
         out = np.empty((n_rows, n_chains, self.dim), dtype=self.dtype)
         _lib.check(self.owner._lib.gm_copy_sample_block(self.owner._h, row0, n_rows, chain0, n_chains,
                                                         _lib.ptr(out)))
         return out
 
     def split_rhat_ess(self):
+        self._check_live()
         return split_rhat_mean_ess_device(self.ptr, self.dtype, self.n_chains, self.n_collect,
                                           self.dim, (self.dim, self.n_chains * self.dim, 1))
 
@@ -59,6 +70,7 @@ class Sampler:
         del keep
         self._h = h
         self._lib = lib
+        self._gen = 0  # incremented by every run: DeviceSamples of older runs are stale
 
     # -- lifetime ---------------------------------------------------------
     def close(self):
@@ -89,13 +101,15 @@ class Sampler:
     def run(self, n_collect: int, n_discard: int) -> np.ndarray:
         """[n_chains, n_collect, dim] on the host."""
         out = np.empty((self.n_chains, n_collect, self.dim), dtype=self.dtype)
+        self._gen += 1
         _lib.check(self._lib.gm_run(self._h, n_collect, n_discard, _lib.ptr(out)))
         return out
 
     def run_positions(self, n_collect: int, n_discard: int) -> DeviceSamples:
         p = C.c_void_p()
+        self._gen += 1
         _lib.check(self._lib.gm_run_device(self._h, n_collect, n_discard, C.byref(p)))
-        return DeviceSamples(p.value or 0, n_collect, self.n_chains, self.dim, self.dtype, self)
+        return DeviceSamples(p.value or 0, n_collect, self.n_chains, self.dim, self.dtype, self, self._gen)
 
     _progress_prefix = "Sampler"
     _progress_interval = 1.0
@@ -120,6 +134,7 @@ class Sampler:
             cb = _lib.PROGRESS_FN(_cb)
         iv = self._progress_interval if interval is None else float(interval)
         stats = None
+        self._gen += 1
         if n_collect >= 2:
             rhat = np.empty(self.dim, dtype=np.float32)
             ess = np.empty(self.dim, dtype=np.float32)
@@ -143,9 +158,10 @@ class Sampler:
         return ChainStats(int(n.value), p, m, v)
 
     def copy_samples(self, n_collect: int) -> np.ndarray:
-        """Samples of the last run, [n_chains, n_collect, dim] on the host."""
+        """Samples of the last run, [n_chains, n_collect, dim] on the host
+        (n_collect must be that run's: the library rejects a mismatch)."""
         out = np.empty((self.n_chains, n_collect, self.dim), dtype=self.dtype)
-        _lib.check(self._lib.gm_copy_samples(self._h, _lib.ptr(out)))
+        _lib.check(self._lib.gm_copy_samples(self._h, n_collect, _lib.ptr(out)))
         return out
 
     def positions(self) -> np.ndarray:

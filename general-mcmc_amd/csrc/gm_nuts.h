@@ -48,7 +48,9 @@ void nuts_free_state(NutsState* ns);
 // Called after each launch with the transitions done so far in the run (the
 // launch may still be in flight); non-zero aborts the run with that status.
 using StepHook = std::function<int(long long)>;
-// progress = 0: NUTS::run semantics; 1: run_progress semantics (see gmcmc.h)
+// progress = 0: NUTS::run semantics; 1: run_progress semantics (see gmcmc.h);
+// 2: NUTS::step, `total` transitions continuing the state (no init, nothing
+// collected, n_discard ignored: the last run's)
 int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay, void* q,
              long long* accepts, void* samples, long long C, int D, double target_accept,
              uint64_t seed, uint64_t* step, uint32_t chain_offset, long long total,

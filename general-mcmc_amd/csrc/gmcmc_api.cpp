@@ -563,7 +563,8 @@ int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems) {
 
 int gm_sampler_set_steps_per_launch(gm_sampler* s, int64_t steps) {
   GM_REQ(s, "sampler is NULL");
-  GM_REQ(steps >= 1, "steps must be >= 1");
+  // the kernels take a launch's transition count as an int
+  GM_REQ(steps >= 1 && steps <= INT32_MAX, "steps must be in [1, 2^31 - 1]");
   s->steps_per_launch = steps;
   return GM_OK;
 }
@@ -795,8 +796,7 @@ static int stage_to_host(gm_sampler* s, void* out, const void* dsrc, size_t byte
   return GM_OK;
 }
 
-int gm_copy_samples(gm_sampler* s, void* out) {
-  GM_REQ(s && out, "bad arguments");
+static int copy_samples_impl(gm_sampler* s, void* out) {
   GM_HIP(hipSetDevice(s->device));
   const long long n_collect = s->last_rows;
   if (n_collect == 0) return GM_OK;
@@ -810,6 +810,15 @@ int gm_copy_samples(gm_sampler* s, void* out) {
     return GM_EHIP;
   }
   return stage_to_host(s, out, s->d_tmp, bytes);
+}
+
+int gm_copy_samples(gm_sampler* s, int64_t n_rows, void* out) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(n_rows == s->last_rows,
+         "n_rows does not match the last run's n_collect (" + std::to_string(s->last_rows) + ")");
+  if (n_rows == 0) return GM_OK;
+  GM_REQ(out != nullptr, "out is NULL");
+  return copy_samples_impl(s, out);
 }
 
 int gm_copy_sample_block(gm_sampler* s, int64_t row0, int64_t n_rows, int64_t chain0, int64_t n_chains,
@@ -831,7 +840,7 @@ int gm_run(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out) {
   int rc = run_impl(s, n_collect, n_discard, 0);
   if (rc) return rc;
   if (!out || n_collect == 0) return GM_OK;
-  return gm_copy_samples(s, out);
+  return copy_samples_impl(s, out);
 }
 
 static float max_skipnan(const float* v, long long n) {  // stats.rs:154-161
@@ -935,7 +944,7 @@ int gm_run_progress_cb(gm_sampler* s, int64_t n_collect, int64_t n_discard, void
     s->trk_n = (unsigned long long)total;
   }
   if (out && n_collect > 0) {
-    rc = gm_copy_samples(s, out);
+    rc = copy_samples_impl(s, out);
     if (rc) return rc;
   }
   if (rhat_out || ess_out) {
@@ -979,9 +988,15 @@ int gm_sampler_chain_stats(gm_sampler* s, uint64_t* n, float* p_accept, float* m
   return GM_OK;
 }
 
+// HMC::step (hmc.rs:316-330), ChainRunner's step (core.rs:81), NUTS::step
+// (nuts.rs:431-433 -> generic_nuts.rs:755-925): one transition of every chain,
+// nothing collected. A NUTS step continues the adaptation counter of the last
+// run (dual averaging only while m <= that run's n_discard, which a step past a
+// completed run never is; then eps = eps_bar) and does not re-run
+// init_chain_state, exactly as the reference's step() does.
 int gm_step(gm_sampler* s) {
   GM_REQ(s, "sampler is NULL");
-  return run_steps(s, 1, 1, 0);
+  return run_steps(s, 1, 1, s->kind == K_NUTS ? 2 : 0);
 }
 
 int gm_get_positions(gm_sampler* s, void* out) {
@@ -1058,9 +1073,13 @@ int gm_nuts_get_mass(gm_sampler* s, int32_t* mode, int32_t* kind, void* dinv, vo
 // state plus the Philox stream position, so a restored sampler continues bit
 // for bit (runs start at init_chain_state, so NUTS needs no mid-trajectory
 // state; HMC and MH re-evaluate logp at every launch start).
+}  // extern "C"
+
 namespace {
+// v2 header: the sampler's configuration too, so that a blob is only loaded
+// into a sampler that would continue it with the same semantics
 struct StateHeader {
-  char magic[8];  // "GMCMCST1"
+  char magic[8];  // "GMCMCST2"
   int32_t kind, dtype;
   int64_t C, D;
   uint64_t seed, step;
@@ -1069,12 +1088,20 @@ struct StateHeader {
   int32_t mass_mode;
   int64_t m_sb, m_eb, sched_next, sched_len;
   double m_reg, m_jit;
+  // configuration (checked on load): HMC eps / L, MH proposal std, NUTS
+  // target accept / max depth, and the NUTS run position (m, n_discard)
+  double eps, prop_std, target_accept;
+  int32_t L, max_depth;
+  int64_t nuts_m, nuts_n_discard;
 };
 struct StatePart {
   void* dev;
   size_t bytes;
 };
-std::vector<StatePart> state_parts(gm_sampler* s) {
+// the blob's parts for a sampler of this kind / shape / metric mode; sizes
+// only depend on the header fields, so a blob can be validated before any
+// state is touched
+std::vector<StatePart> state_parts_for(gm_sampler* s, int mass_mode) {
   const size_t C = (size_t)s->C, D = (size_t)s->D, e = s->esz;
   std::vector<StatePart> v{{s->d_q, C * D * e}, {s->d_acc, C * sizeof(long long)}};
   if (s->kind == K_NUTS) {
@@ -1084,24 +1111,27 @@ std::vector<StatePart> state_parts(gm_sampler* s) {
     v.push_back({n.h_bar, C * e});
     v.push_back({n.mu, C * e});
     v.push_back({n.n_leapfrog, C * sizeof(long long)});
-    if (n.mass_mode) {
+    if (mass_mode) {
       v.push_back({n.mkind, C * sizeof(int)});
       v.push_back({n.dinv, C * D * e});
       v.push_back({n.dsq, C * D * e});
     }
-    if (n.mass_mode == 2) {
+    if (mass_mode == 2) {
       v.push_back({n.minv, C * D * D * e});
       v.push_back({n.mchol, C * D * D * e});
     }
   }
   return v;
 }
-size_t state_bytes(gm_sampler* s) {
+size_t parts_bytes(const std::vector<StatePart>& v) {
   size_t b = sizeof(StateHeader);
-  for (auto& p : state_parts(s)) b += p.bytes;
+  for (auto& p : v) b += p.bytes;
   return b;
 }
+size_t state_bytes(gm_sampler* s) { return parts_bytes(state_parts_for(s, s->kind == K_NUTS ? s->nuts.mass_mode : 0)); }
 }  // namespace
+
+extern "C" {
 
 int gm_state_size(gm_sampler* s, uint64_t* bytes) {
   GM_REQ(s && bytes, "bad arguments");
@@ -1116,7 +1146,7 @@ int gm_state_save(gm_sampler* s, void* out, uint64_t bytes) {
   GM_HIP(hipStreamSynchronize(s->stream));
   StateHeader h;
   memset(&h, 0, sizeof(h));
-  memcpy(h.magic, "GMCMCST1", 8);
+  memcpy(h.magic, "GMCMCST2", 8);
   h.kind = s->kind;
   h.dtype = s->dt;
   h.C = s->C;
@@ -1125,6 +1155,11 @@ int gm_state_save(gm_sampler* s, void* out, uint64_t bytes) {
   h.step = s->step;
   h.total_steps = s->total_steps;
   h.chain_offset = s->chain_offset;
+  h.eps = s->eps;
+  h.L = s->L;
+  h.prop_std = s->prop_std;
+  h.target_accept = s->target_accept;
+  h.max_depth = s->max_depth;
   if (s->kind == K_NUTS) {
     const NutsState& n = s->nuts;
     h.mass_mode = n.mass_mode;
@@ -1134,40 +1169,55 @@ int gm_state_save(gm_sampler* s, void* out, uint64_t bytes) {
     h.sched_len = n.sched_len;
     h.m_reg = n.m_reg;
     h.m_jit = n.m_jit;
+    h.nuts_m = n.m;
+    h.nuts_n_discard = n.n_discard;
   }
   unsigned char* o = (unsigned char*)out;
   memcpy(o, &h, sizeof(h));
   o += sizeof(h);
-  for (auto& p : state_parts(s)) {
+  for (auto& p : state_parts_for(s, h.mass_mode)) {
     GM_HIP(hipMemcpy(o, p.dev, p.bytes, hipMemcpyDeviceToHost));
     o += p.bytes;
   }
   return GM_OK;
 }
 
+// Every check happens before the sampler is changed: a truncated, corrupt or
+// foreign blob returns GM_EINVAL and leaves the sampler as it was.
 int gm_state_load(gm_sampler* s, const void* in, uint64_t bytes) {
   GM_REQ(s && in, "bad arguments");
   GM_REQ(bytes >= sizeof(StateHeader), "state blob too short");
   StateHeader h;
   memcpy(&h, in, sizeof(h));
-  GM_REQ(memcmp(h.magic, "GMCMCST1", 8) == 0, "not a libgmcmc state blob");
+  GM_REQ(memcmp(h.magic, "GMCMCST2", 8) == 0, "not a libgmcmc state blob (v2)");
   GM_REQ(h.kind == s->kind && h.dtype == (int32_t)s->dt && h.C == s->C && h.D == s->D &&
              h.chain_offset == s->chain_offset,
          "state blob is for a different sampler kind, dtype, shape or chain offset");
+  switch (s->kind) {
+    case K_HMC:
+      GM_REQ(h.eps == s->eps && h.L == s->L, "state blob is for a different step size / n_leapfrog");
+      break;
+    case K_MH:
+      GM_REQ(h.prop_std == s->prop_std, "state blob is for a different proposal std");
+      break;
+    case K_NUTS:
+      GM_REQ(h.target_accept == s->target_accept && h.max_depth == s->max_depth,
+             "state blob is for a different target_accept_p / max_depth");
+      GM_REQ(h.mass_mode >= 0 && h.mass_mode <= 2, "corrupt state blob (mass mode)");
+      GM_REQ(h.nuts_m >= 0 && h.nuts_n_discard >= 0 && h.sched_len >= 0, "corrupt state blob (counters)");
+      break;
+  }
+  if (s->kind != K_NUTS) GM_REQ(h.mass_mode == 0, "corrupt state blob (mass mode)");
+  GM_REQ(bytes >= parts_bytes(state_parts_for(s, h.mass_mode)), "state blob too short");
   GM_HIP(hipSetDevice(s->device));
   GM_HIP(hipStreamSynchronize(s->stream));
-  if (s->kind == K_NUTS) {
-    GM_REQ(h.mass_mode >= 0 && h.mass_mode <= 2, "corrupt state blob");
-    if (h.mass_mode != s->nuts.mass_mode || h.mass_mode) {
-      const int rc = nuts_set_mass(&s->nuts, s->dt, s->C, s->D, h.mass_mode, h.m_sb, h.m_eb, 0,
-                                   h.m_reg, h.m_jit);
-      if (rc) return rc;
-    }
+  if (s->kind == K_NUTS && (h.mass_mode != s->nuts.mass_mode || h.mass_mode)) {
+    const int rc = nuts_set_mass(&s->nuts, s->dt, s->C, s->D, h.mass_mode, h.m_sb, h.m_eb, 0,
+                                 h.m_reg, h.m_jit);
+    if (rc) return rc;
   }
-  // the parts' sizes follow from the (now matching) sampler
-  GM_REQ(bytes >= state_bytes(s), "state blob too short");
   const unsigned char* p = (const unsigned char*)in + sizeof(h);
-  for (auto& part : state_parts(s)) {
+  for (auto& part : state_parts_for(s, h.mass_mode)) {
     GM_HIP(hipMemcpy(part.dev, p, part.bytes, hipMemcpyHostToDevice));
     p += part.bytes;
   }
@@ -1177,6 +1227,8 @@ int gm_state_load(gm_sampler* s, const void* in, uint64_t bytes) {
   if (s->kind == K_NUTS) {
     s->nuts.sched_next = h.sched_next;
     s->nuts.sched_len = h.sched_len;
+    s->nuts.m = h.nuts_m;
+    s->nuts.n_discard = h.nuts_n_discard;
   }
   return GM_OK;
 }

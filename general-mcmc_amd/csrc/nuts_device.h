@@ -418,7 +418,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   }
   auto record = [&](long long t) {
     const long long row = t - a.row_shift;
-    if (row >= 0 && row < a.n_rows) {
+    if (row >= 0 && row < a.n_rows && a.samples != nullptr) {
       T* __restrict__ out = (T*)a.samples + (row * C + c) * D;
 #pragma unroll
       for (int e = 0; e < E; ++e) {

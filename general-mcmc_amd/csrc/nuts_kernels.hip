@@ -322,11 +322,17 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     }
     ns.stk_lanes = lanes_total;
   }
-  // init_chain_state at the start of every run (generic_nuts.rs:731-753)
-  ns.m = 0;
-  ns.n_discard = n_discard;
+  // progress == 2: NUTS::step (nuts.rs:431-433 -> generic_nuts.rs:755-925):
+  // transitions that continue the chain state without init_chain_state, the
+  // adaptation counter running on against the last run's n_discard, nothing
+  // collected
+  const bool step_mode = progress == 2;
+  if (!step_mode) {  // init_chain_state at the start of every run (generic_nuts.rs:731-753)
+    ns.m = 0;
+    ns.n_discard = n_discard;
+  }
   const uint64_t init_step = *step;
-  const long long n_rows_total = progress ? total - n_discard : total - n_discard + 1;
+  const long long n_rows_total = step_mode ? 0 : progress ? total - n_discard : total - n_discard + 1;
   const long long row_shift = progress ? n_discard + 1 : n_discard;
   // Launch segments: at most steps_per_launch transitions each, and a
   // segment also ends at every warm-up window end, after which the metric
@@ -338,7 +344,7 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
   std::vector<char> seg_update;
   {
     std::vector<long long> wends;
-    if (ns.mass_mode) {
+    if (ns.mass_mode && !step_mode) {  // (a step runs past the warm-up: m > n_discard)
       const long long lim = n_discard > ns.m_eb ? n_discard - ns.m_eb : 0;
       for (long long m = 1; m <= total && m <= n_discard; ++m) {
         if (m <= ns.m_sb || !(m < lim)) continue;  // should_collect
@@ -380,7 +386,7 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     }
     evs.push_back(ev);
   }
-  if (ns.mass_mode) {  // RunningCov::reset in init_chain_state (:744-746)
+  if (ns.mass_mode && !step_mode) {  // RunningCov::reset in init_chain_state (:744-746)
     hipMemsetAsync(ns.rn, 0, C * sizeof(int), st);
     hipMemsetAsync(ns.rmean, 0, (size_t)C * D * esz, st);
     hipMemsetAsync(ns.rm2d, 0, (size_t)C * D * esz, st);
@@ -424,8 +430,8 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     a.chain_offset = chain_offset;
     a.n_steps = (int)nst;
     a.m0 = ns.m + start;
-    a.n_discard = n_discard;
-    a.do_init = (start == 0 && li == 0) ? 1 : 0;
+    a.n_discard = ns.n_discard;
+    a.do_init = (!step_mode && start == 0 && li == 0) ? 1 : 0;
     a.t0 = start;
     a.row_shift = row_shift;
     a.n_rows = n_rows_total > 0 ? n_rows_total : 0;
@@ -516,7 +522,7 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     }
   }
   ns.m += total;
-  *step += (uint64_t)total + 1;  // +1: the init draw consumed a counter value
+  *step += (uint64_t)total + (step_mode ? 0 : 1);  // +1: the init draw consumed a counter value
   hipError_t e = hipStreamSynchronize(st);
   if (e != hipSuccess) {
     set_error(std::string("NUTS run failed: ") + hipGetErrorString(e));

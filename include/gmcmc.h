@@ -173,17 +173,19 @@ int gm_run_progress(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* o
                     float* rhat_out, float* ess_out);
 
 /* Copy the samples of the last run (device [n_collect][n_chains][dim]) to host
- * in the reference layout [n_chains][n_collect][dim]. */
-int gm_copy_samples(gm_sampler* s, void* out);
+ * in the reference layout [n_chains][n_collect][dim]. n_rows must equal that
+ * run's n_collect (the size of `out` in rows): GM_EINVAL otherwise, so a
+ * buffer sized for an earlier, smaller run is never overrun. */
+int gm_copy_samples(gm_sampler* s, int64_t n_rows, void* out);
 
-/* positions() (hmc.rs:326-328): host [n_chains][dim]. */
 /* A block of the last run's device samples, rows [row0, row0+n_rows) x
  * chains [chain0, chain0+n_chains), copied to the host as
  * [n_rows][n_chains][dim] (one strided copy): the streaming egress used by
- * the CSV / Arrow / Parquet writers (io/*.rs) so that a sample larger than
+ * the CSV / Arrow / Parquet writers (io/csv.rs, io/arrow.rs, io/parquet.rs) so that a sample larger than
  * host memory never has to exist there whole. */
 int gm_copy_sample_block(gm_sampler* s, int64_t row0, int64_t n_rows, int64_t chain0, int64_t n_chains,
                          void* out);
+/* positions() (hmc.rs:326-328): host [n_chains][dim]. */
 int gm_get_positions(gm_sampler* s, void* out);
 int gm_set_positions(gm_sampler* s, const void* in);
 

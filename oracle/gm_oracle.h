@@ -91,6 +91,19 @@ int or_nuts_run_f(const or_target* t, int lanes, int elems, int64_t C, int D, fl
                   int max_depth, uint64_t seed, uint64_t init_step, uint32_t chain_offset,
                   int64_t n_collect, int64_t n_discard, int progress, float* samples,
                   int64_t* accepts, int64_t* n_leapfrog, int threads);
+/* NUTS::step (nuts.rs:431-433 -> generic_nuts.rs:755-925): n_steps
+ * transitions without init_chain_state, adaptation counter from m0 against
+ * n_discard, transition s drawing at counter step0 + s; nothing collected. */
+int or_nuts_step_d(const or_target* t, int lanes, int elems, int64_t C, int D, double* q,
+                   double* eps, double* eps_bar, double* h_bar, double* mu, double target_accept,
+                   int max_depth, uint64_t seed, uint64_t step0, uint32_t chain_offset,
+                   int64_t n_steps, int64_t m0, int64_t n_discard, int64_t* accepts,
+                   int64_t* n_leapfrog, int threads);
+int or_nuts_step_f(const or_target* t, int lanes, int elems, int64_t C, int D, float* q,
+                   float* eps, float* eps_bar, float* h_bar, float* mu, double target_accept,
+                   int max_depth, uint64_t seed, uint64_t step0, uint32_t chain_offset,
+                   int64_t n_steps, int64_t m0, int64_t n_discard, int64_t* accepts,
+                   int64_t* n_leapfrog, int threads);
 /* ---- NUTS mass-matrix warmup (generic_nuts.rs:33-359, 897-921) ----
  * GenericNUTS::new_with_mass_matrix: Welford windows during warm-up, the
  * diagonal or dense metric, the probe + find_reasonable_epsilon re-start

@@ -59,6 +59,9 @@ def load():
         getattr(lib, f"or_nuts_run_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _vp, _vp,
                                                        _vp, _vp, _dbl, _int, _u64, _u64, _u32,
                                                        _i64, _i64, _int, _vp, _vp, _vp, _int]
+        getattr(lib, f"or_nuts_step_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _vp, _vp,
+                                                        _vp, _vp, _dbl, _int, _u64, _u64, _u32,
+                                                        _i64, _i64, _i64, _vp, _vp, _int]
     for sfx in ("d", "f"):
         getattr(lib, f"or_nuts_mass_run_{sfx}").argtypes = [
             tp, _int, _int, _i64, _int, _vp, _vp, _vp, _vp, _vp, _dbl, _int, _u64, _u64, _u32, _i64,
@@ -220,6 +223,21 @@ class Oracle:
             threads)
         assert rc == 0
         return q, samples, acc, nlf
+
+    def nuts_step(self, target: Target, q, state, target_accept, max_depth, seed, step0, n_steps,
+                  m0, n_discard, lanes, elems, chain_offset=0, threads=8):
+        """NUTS::step n_steps times (no init_chain_state, nothing collected)."""
+        q = np.array(q, copy=True, order="C")
+        C_, D = q.shape
+        acc = np.zeros(C_, dtype=np.int64)
+        nlf = np.zeros(C_, dtype=np.int64)
+        t = target.struct()
+        rc = getattr(self.lib, f"or_nuts_step_{_sfx(q.dtype)}")(
+            C.byref(t), lanes, elems, C_, D, _p(q), _p(state["eps"]), _p(state["eps_bar"]),
+            _p(state["h_bar"]), _p(state["mu"]), target_accept, max_depth, seed, step0,
+            chain_offset, n_steps, m0, n_discard, _p(acc), _p(nlf), threads)
+        assert rc == 0
+        return q, acc, nlf
 
     def split_rhat_ess(self, x):
         x = np.ascontiguousarray(x, dtype=np.float32)

@@ -105,3 +105,38 @@ def test_state_mismatch_raises(gm):
         a.load_state(b"not a state blob" * 8)
     with pytest.raises(gm.GMError):
         a.load_state(blob[:40])
+
+
+def test_state_config_mismatch_raises(gm):
+    x0 = gm.init_det(4, 3, np.float32)
+    blob = gm.HMC(gm.RosenbrockND(), x0, 0.01, 3).save_state()
+    with pytest.raises(gm.GMError):  # another step size
+        gm.HMC(gm.RosenbrockND(), x0, 0.02, 3).load_state(blob)
+    with pytest.raises(gm.GMError):  # another n_leapfrog
+        gm.HMC(gm.RosenbrockND(), x0, 0.01, 4).load_state(blob)
+    nb = gm.NUTS(gm.RosenbrockND(), x0, 0.8, max_depth=6).save_state()
+    with pytest.raises(gm.GMError):  # another max_depth
+        gm.NUTS(gm.RosenbrockND(), x0, 0.8, max_depth=7).load_state(nb)
+    with pytest.raises(gm.GMError):  # another target_accept_p
+        gm.NUTS(gm.RosenbrockND(), x0, 0.7, max_depth=6).load_state(nb)
+
+
+def test_truncated_mass_blob_leaves_sampler_unchanged(gm):
+    """A truncated or corrupt NUTS blob is rejected before anything is changed
+    (the learned metric and the positions stay)."""
+    t = gm.DenseGaussian(np.zeros(4), np.diag([2.0, 1.0, 0.2, 4.0]))
+    x0 = gm.init_with_seed(8, 4, 6)
+    cfg = gm.NUTSMassMatrixConfig("dense", start_buffer=5, end_buffer=5, initial_window=10)
+    a = gm.NUTS.new_with_mass_matrix(t, x0, 0.8, cfg).set_seed(2)
+    a.run(3, 40)
+    blob = a.save_state()
+    before = (a.positions(), a.mass_matrix(), a.step_sizes())
+    for bad in (blob[:len(blob) // 2], blob[:-8]):
+        with pytest.raises(gm.GMError):
+            a.load_state(bad)
+        after = (a.positions(), a.mass_matrix(), a.step_sizes())
+        np.testing.assert_array_equal(before[0], after[0])
+        np.testing.assert_array_equal(before[1].kind, after[1].kind)
+        np.testing.assert_array_equal(before[1].dense_inv, after[1].dense_inv)
+        np.testing.assert_array_equal(before[2][0], after[2][0])
+    a.load_state(blob)  # the intact blob still loads
