@@ -5,18 +5,24 @@ high-dimensional Rosenbrock settings, hmc.rs:763-780).
 A "step" is one HMC transition of every chain (L leapfrogs each). The timed
 region runs --steps transitions with every state collected on the device,
 bracketed by a barrier and a device synchronize on both sides; the time is
-the maximum over ranks. Then the split-R-hat / ESS of the collected draws is
-computed on the GPUs (RCCL all-gather of per-split-chain summaries when N > 1).
+the maximum over ranks. The split-R-hat / ESS of those draws follows (RCCL
+all-gather of per-split-chain summaries when N > 1), and a separately timed
+ESS leg runs cfg2's own schedule (n_discard 100, n_collect 100; hmc.rs:763-780)
+from the same start, so that ESS/s does not depend on --steps/--warmup.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Prints one JSON line (rank 0).
+Prints one JSON line (rank 0). Every field of the N = 1 line is also in the
+N > 1 line: the rank-0-only measurements (copy ceiling, per-leapfrog HBM
+kernel, host-output path, CPU baseline) run on rank 0 after the timed region
+while the other ranks wait at the closing barrier.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -27,10 +33,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
-VALU_F32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (spec)
+VALU_F32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md, spec)
+METRIC = "leapfrog steps/sec (whole node) + ESS/sec, 64-dim Rosenbrock HMC at 1/2/4/8 GPUs"
+PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_hmc.json")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
@@ -41,111 +49,389 @@ def parse():
     p.add_argument("--eps", type=float, default=0.01)
     p.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     p.add_argument("--layout", default="", help="lanes,elems override")
+    p.add_argument("--ess-discard", type=int, default=100, help="ESS leg burn-in (cfg2: 100)")
+    p.add_argument("--ess-collect", type=int, default=100, help="ESS leg draws (cfg2: 100)")
+    p.add_argument("--ess-long-discard", type=int, default=4000,
+                   help="second ESS leg: long burn-in toward stationarity (0 disables)")
+    p.add_argument("--ess-long-collect", type=int, default=1000)
     p.add_argument("--cpu-seconds", type=float, default=12.0,
-                   help="target CPU time of the oracle baseline sample (0 disables)")
-    p.add_argument("--cpu-threads", type=int, default=0)
+                   help="target CPU time of each CPU-baseline sample (0 disables)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0: every core available to this process")
     p.add_argument("--north-star", action="store_true",
                    help="also time BASELINE.json north_star's 16384-chain shape (off by default, so that "
                         "every hmc_kernel launch of the default run has the bench's shape)")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def main():
-    a = parse()
-    import general_mcmc_amd as gm
-    from general_mcmc_amd import _lib
-    from general_mcmc_amd.distributed import Comm, ControlPlane, shard
+def f_alg_rosenbrock(D):
+    """RosenbrockND logp+grad ~15 flops per coupled pair, two
+    kicks and a drift 6 per coordinate: flops per chain-leapfrog."""
+    return 15 * (D - 1) + 6 * D
+
+
+def b_step(D, L, s_bytes):
+    """SURVEY 8(d) / BASELINE.md algorithmic bytes per chain-transition of
+    the per-leapfrog (state in HBM) formulation, collected step."""
+    return (L * (6 * D + 1) + (4 * D + 2) + D) * s_bytes
+
+
+# --------------------------------------------------------------------------
+# The GPU side (libgmcmc through the Python facade). The test suite replaces
+# this class with a stub to run main()'s aggregation and JSON assembly under
+# gloo with world_size 2 on the CPU (tests/test_bench_cpu.py).
+class GpuBench:
+    def __init__(self, a, cp):
+        import general_mcmc_amd as gm
+        from general_mcmc_amd import _lib
+        self.gm, self._lib, self.a, self.cp = gm, _lib, a, cp
+        lib = _lib.load()
+        _lib.check(lib.gm_set_device(cp.local_rank))
+        self.lib = _lib.require_gpu()
+        self.dtype = np.float32 if a.dtype == "f32" else np.float64
+
+    def init_positions(self, n, offset, count):
+        return self.gm.init_with_seed(n, self.a.dim, 42, np.float64)[offset:offset + count].astype(self.dtype)
+
+    def sampler(self, x0, offset):
+        a = self.a
+        s = self.gm.HMC(self.gm.RosenbrockND(), x0, a.eps, a.leapfrog, dtype=self.dtype,
+                        chain_offset=offset).set_seed(42)
+        if a.layout:
+            s.set_layout(*[int(v) for v in a.layout.split(",")])
+        return s
+
+    def sync(self):
+        self._lib.check(self.lib.gm_device_synchronize())
+
+    def comm(self):
+        from general_mcmc_amd.distributed import Comm
+        return Comm(self.cp, self.lib) if self.cp.world > 1 else None
+
+    def diagnostics(self, ds, comm):
+        return comm.split_rhat_ess(ds) if comm is not None else ds.split_rhat_ess()
+
+    def copy_ceiling(self, nbytes=1 << 30, reps=5):
+        """Empirical HBM ceiling on this box: a 1 GiB
+        device-to-device copy, read + write bytes over the median time."""
+        import ctypes as C
+        lib, _lib = self.lib, self._lib
+        src, dst = C.c_void_p(), C.c_void_p()
+        try:
+            _lib.check(lib.gm_malloc(C.byref(src), nbytes))
+            _lib.check(lib.gm_malloc(C.byref(dst), nbytes))
+            ts = []
+            for _ in range(reps + 1):
+                _lib.check(lib.gm_device_synchronize())
+                t0 = time.perf_counter()
+                _lib.check(lib.gm_memcpy_dtod(dst, src, nbytes))
+                _lib.check(lib.gm_device_synchronize())
+                ts.append(time.perf_counter() - t0)
+            return 2 * nbytes / float(np.median(ts[1:])) / 1e9
+        except Exception:
+            return None
+        finally:
+            for p in (src, dst):
+                if p.value:
+                    lib.gm_free(p)
+
+    def per_leapfrog_hbm(self, chains=1 << 20, reps=20):
+        """The unfused, per-leapfrog design the HBM roofline is written for
+        (SURVEY.md 8(d)): gm_bv_leapfrog, one kernel per leapfrog with q, p,
+        g and logp in HBM, at an HBM-resident size (2^20 chains: 256 MiB per
+        array); achieved = B_alg (6D+1)*s per chain-leapfrog x chains / time."""
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        try:
+            from hbm_leapfrog import measure
+            r = measure(chains, self.a.dim, self.dtype, reps)
+        except Exception as e:  # reported, never fatal to the bench line
+            return {"error": str(e)}
+        return {"kernel": "leapfrog_hbm_kernel", "chains": chains, "achieved": r["achieved_gbs"],
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": r["hbm_frac"],
+                "us_per_leapfrog": r["us_per_leapfrog"], "chain_leapfrogs_per_s": r["chain_leapfrogs_per_s"]}
+
+    def host_output(self, sampler):
+        """The same transitions through gm_run (HMC::run, hmc.rs:164-181):
+        the [C, N, D] sample returned in a host array (device transpose + D2H
+        into pageable memory). The PCIe-inclusive rate; never `value`."""
+        a = self.a
+        sampler.run(a.steps, 0)  # warm (host array, staging buffers)
+        self.sync()
+        t0 = time.perf_counter()
+        out = sampler.run(a.steps, 0)
+        t = time.perf_counter() - t0
+        C, N, D = out.shape
+        return {"chain_leapfrogs_per_s": C * a.leapfrog * N / t, "seconds": t,
+                "sample_bytes": int(out.nbytes), "d2h_gbs_incl_sampling": out.nbytes / t / 1e9}
+
+    def ess_leg(self, x0, offset, comm, n_discard, n_collect):
+        """cfg2's schedule from the bench's start: a fresh sampler,
+        run_positions(n_collect, n_discard) timed (burn-in included, as the
+        reference's run(100, 100)), then the device diagnostics timed on
+        their own. Returns this rank's times; the caller takes the max."""
+        s = self.sampler(x0, offset)
+        try:
+            s.reserve(n_collect)
+            self.sync()
+            self.cp.barrier()
+            t0 = time.perf_counter()
+            ds = s.run_positions(n_collect, n_discard)
+            self.sync()
+            t_sample = time.perf_counter() - t0
+            self.cp.barrier()
+            t0 = time.perf_counter()
+            rhat, ess = self.diagnostics(ds, comm)
+            t_diag = time.perf_counter() - t0
+        finally:
+            s.close()
+        return t_sample, t_diag, rhat, ess
+
+    def north_star_check(self, chains=16384):
+        """BASELINE.json north_star's target shape: >= 10^4 chains of 64-D
+        Rosenbrock HMC on one GPU (device time of one launch)."""
+        a, gm = self.a, self.gm
+        D, L, n = a.dim, a.leapfrog, 100
+        s = gm.HMC(gm.RosenbrockND(), gm.init_with_seed(chains, D, 43, np.float64).astype(self.dtype),
+                   a.eps, L, dtype=self.dtype).set_seed(43)
+        try:
+            s.reserve(n)
+            s.run_positions(0, 20)
+            s.run_positions(n, 0)
+            ms, launches = s.last_run_stats()
+        finally:
+            s.close()
+        flops = f_alg_rosenbrock(D) * chains * L * n / (ms * 1e-3) / 1e12
+        return {"chains": chains, "chain_leapfrogs_per_s": chains * L * n / (ms * 1e-3),
+                "launch_ms": ms / max(launches, 1), "valu_tflops": flops,
+                "valu_frac": flops / VALU_F32_PEAK_TFLOPS}
+
+    def cpu_baseline(self, x0, lanes, elems):
+        return cpu_baseline(self.a, self.dtype, x0, lanes, elems)
+
+
+# --------------------------------------------------------------------------
+def available_cores():
+    """Cores this process may use, with the evidence: the affinity mask and
+    the cgroup v2 (or v1) CPU quota; the smaller bounds the thread count."""
+    ev = {}
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    ev["sched_getaffinity"] = aff
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            ev["cgroup_cpu_max"] = f"{q} {per}"
+            if q != "max":
+                quota = float(q) / float(per)
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            ev["cgroup_v1_cfs"] = f"{q} {per}"
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    ev["cgroup_quota_cores"] = quota
+    ev["os_cpu_count"] = os.cpu_count()
+    ev["OMP_NUM_THREADS"] = os.environ.get("OMP_NUM_THREADS")
+    n = aff if quota is None else max(1, min(aff, int(math.floor(quota))))
+    return n, ev
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(a, dtype, x0, lanes, elems):
+    """The reference's CPU path timed on this host's available cores, on a
+    bounded sample of the same workload (all chains, as many transitions as
+    fit in about --cpu-seconds each):
+      * value: oracle/cpu_hmc.c, a restatement of batched_hmc.rs's step with
+        the reference's operation structure (one pass per BatchVector op over
+        a chain block, left-to-right sums, euclidean.rs:392-394/447-534),
+        gcc -O3 -march=native, threads over chain blocks like rayon's
+        par_iter (core.rs:221-225). Not bit-matching (its own momentum
+        stream: xoshiro256++ + Box-Muller, the reference's SmallRng family).
+      * oracle: the bit-matching C oracle (gcc -O2 -ffp-contract=off, the
+        engine's 64-lane summation order), for context."""
+    from tests import _oracle
+    threads, ev = available_cores()
+    if a.cpu_threads:
+        threads = a.cpu_threads
+    C = x0.shape[0]
+    out = {"unit": "chain-leapfrog steps/s", "cores": threads, "kind": "port",
+           "host": {"cpu_model": _cpu_model(), **ev}}
+    fast = _oracle.cpu_hmc()
+    if fast is not None and dtype == np.float32:
+        q = np.array(x0, copy=True)
+        fast.run(q, a.eps, a.leapfrog, 1, 42, threads)
+        t0 = time.perf_counter()
+        fast.run(q, a.eps, a.leapfrog, 1, 42, threads)
+        one = time.perf_counter() - t0
+        steps = max(1, int(a.cpu_seconds / max(one, 1e-6)))
+        t0 = time.perf_counter()
+        fast.run(q, a.eps, a.leapfrog, steps, 43, threads)
+        dt = time.perf_counter() - t0
+        out["value"] = C * a.leapfrog * steps / dt
+        out["sample"] = (f"{C} chains x {steps} transitions x {a.leapfrog} leapfrogs, oracle/cpu_hmc.c "
+                         f"(-O3 -march=native, reference op structure), {threads} threads, {dt:.1f}s")
+    ora = _oracle.load()
+    t = _oracle.Target(1, a.dim, a=1.0, b=100.0)
+    q = np.array(x0, copy=True)
+    t0 = time.perf_counter()
+    ora.hmc_run(t, q, a.eps, a.leapfrog, 42, 0, 1, 1, lanes, elems, threads=threads)
+    one = time.perf_counter() - t0
+    steps = max(1, int(a.cpu_seconds / max(one, 1e-6)))
+    t0 = time.perf_counter()
+    ora.hmc_run(t, q, a.eps, a.leapfrog, 42, 1, steps, steps, lanes, elems, threads=threads)
+    dt = time.perf_counter() - t0
+    out["oracle"] = {"value": C * a.leapfrog * steps / dt, "threads": threads,
+                     "sample": f"{C} chains x {steps} transitions, oracle/gm_oracle.c (-O2, bit-matching), {dt:.1f}s"}
+    if "value" not in out:
+        out["value"] = out["oracle"]["value"]
+        out["sample"] = out["oracle"]["sample"]
+    return out
+
+
+def load_pmc(C, D, L, dtype, steps):
+    """PMC figures of the timed hmc_kernel launch from profiles/r02
+    (tools/pmc_hmc.py over rocprofv3 passes of the driver's command). A
+    launch of K transitions moves fixed + K x per-transition bytes; figures
+    for a K that was not profiled are scaled on that line and marked so."""
+    try:
+        d = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None, None
+    e = d.get(f"C{C}_D{D}_L{L}_{dtype}")
+    if not e:
+        return None, None
+    byk = {int(k): v for k, v in e.get("by_steps", {}).items()}
+    traffic = issue = None
+    if steps in byk:
+        r = byk[steps]
+        traffic = {"bytes": r["hbm_bytes_per_launch"], "source": r["source"], "scaled": False}
+        issue = dict(r.get("valu", {}), scaled=False) if r.get("valu") else None
+    elif "fit" in e:
+        f = e["fit"]
+        traffic = {"bytes": f["fixed_bytes"] + f["bytes_per_transition"] * steps,
+                   "source": f["source"], "scaled": True}
+    if issue is None and byk:
+        k = min(byk, key=lambda k: abs(k - steps))
+        if byk[k].get("valu"):
+            issue = dict(byk[k]["valu"], scaled=True, measured_at_steps=k)
+    return traffic, issue
+
+
+def fin(v):
+    """float, or None where undefined (diagnostics need >= 4 draws)."""
+    v = float(v)
+    return v if np.isfinite(v) else None
+
+
+def rhat_block(rhat):
+    r = np.asarray(rhat, dtype=np.float64)
+    stan = 1.0 / r
+    return {"reference_sqrt_W_over_V": {"min": fin(np.min(r)), "max": fin(np.max(r))},
+            "stan_sqrt_V_over_W": {"min": fin(np.min(stan)), "max": fin(np.max(stan))},
+            "max_abs_dev_from_1": fin(np.max(np.abs(stan - 1.0)))}
+
+
+def main(argv=None, backend=None):
+    a = parse(argv)
+    from general_mcmc_amd.distributed import ControlPlane, shard
 
     cp = ControlPlane()  # gloo control plane when launched by torchrun
     world, rank = cp.world, cp.rank
-    lib = _lib.load()
-    _lib.check(lib.gm_set_device(cp.local_rank))
-    lib = _lib.require_gpu()
-
-    dtype = np.float32 if a.dtype == "f32" else np.float64
-    s_bytes = np.dtype(dtype).itemsize
+    be = (backend or GpuBench)(a, cp)
+    s_bytes = 4 if a.dtype == "f32" else 8
     D, L = a.dim, a.leapfrog
     C_glob = a.chains * world
     offset, C_loc = shard(C_glob, world, rank)
-    x0 = gm.init_with_seed(C_glob, D, 42, np.float64)[offset:offset + C_loc].astype(dtype)
-    sampler = gm.HMC(gm.RosenbrockND(), x0, a.eps, L, dtype=dtype, chain_offset=offset).set_seed(42)
-    if a.layout:
-        sampler.set_layout(*[int(v) for v in a.layout.split(",")])
+    x0 = be.init_positions(C_glob, offset, C_loc)
+    sampler = be.sampler(x0, offset)
     lanes, elems = sampler.layout()
-    comm = Comm(cp, lib) if world > 1 else None
+    comm = be.comm()
 
     def barrier_sync():
-        _lib.check(lib.gm_device_synchronize())
+        be.sync()
         cp.barrier()
 
-    # the sample buffer is resident before the clock starts, like the state
-    sampler.reserve(a.steps)
-    # warmup = burn-in transitions (untimed)
+    # the sample buffer is resident before the clock starts, like the state;
+    # the W warm-up transitions collect into it (untimed)
+    sampler.reserve(max(a.steps, a.warmup))
     if a.warmup > 0:
-        sampler.run_positions(0, a.warmup)
+        sampler.run_positions(a.warmup, 0)
     barrier_sync()
     t0 = time.perf_counter()
     ds = sampler.run_positions(a.steps, 0)
     # each rank's clock stops at its own device synchronize; the closing
-    # barrier follows, so its (gloo, host-network) latency is not charged to
-    # the GPU time, and the max over ranks below is the slowest rank's time
-    _lib.check(lib.gm_device_synchronize())
+    # barrier follows, so its (gloo) latency is not charged to the GPU time,
+    # and the max over ranks below is the slowest rank's time
+    be.sync()
     t_local = time.perf_counter() - t0
     cp.barrier()
     kernel_ms, launches = sampler.last_run_stats()
-    t_max, launch_ms = cp.max([t_local, kernel_ms / max(launches, 1)])
+    ranks = cp.gather({"rank": rank, "wall_ms": t_local * 1e3, "kernel_ms": kernel_ms, "launches": launches})
+    t_max = max(r["wall_ms"] for r in ranks) * 1e-3
+    kmax = max(r["kernel_ms"] for r in ranks)
+    launch_ms = max(r["kernel_ms"] / max(r["launches"], 1) for r in ranks)
 
-    # diagnostics on the collected draws (device; RCCL all-gather when N > 1)
+    # diagnostics of the timed draws (device; RCCL all-gather when N > 1)
     td0 = time.perf_counter()
     if a.steps >= 4:
-        rhat, ess = comm.split_rhat_ess(ds) if comm is not None else ds.split_rhat_ess()
+        rhat, ess = be.diagnostics(ds, comm)
     else:
         rhat = ess = np.full(D, np.nan, dtype=np.float32)
     t_diag = time.perf_counter() - td0
 
-    # throughput: chain-leapfrogs per second over the whole job
-    value = C_glob * L * a.steps / t_max
-    # roofline of the dominant kernel: algorithmic bytes per launch (BASELINE.md
-    # "Roofline accounting"): per transition and chain
-    #   B_step = L (6D+1) s + (4D+2) s + D s (collected)
-    b_step = (L * (6 * D + 1) + (4 * D + 2) + D) * s_bytes
-    steps_per_launch = a.steps / max(launches, 1)
-    bytes_per_launch = b_step * C_loc * steps_per_launch
-    achieved_gbs = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-    flops_lf = 15 * (D - 1) + 6 * D  # RosenbrockND logp+grad and kick/drift/kick per chain-leapfrog
-    achieved_tflops = flops_lf * C_loc * L * steps_per_launch / (launch_ms * 1e-3) / 1e12
+    # ESS legs on their own schedules (every rank; diagnostics over all chains)
+    legs = {}
+    for name, nd, nc in (("cfg2_schedule", a.ess_discard, a.ess_collect),
+                         ("long", a.ess_long_discard, a.ess_long_collect)):
+        if nc < 4 or (name == "long" and nd <= 0):
+            continue
+        ts, tdg, rh, es = be.ess_leg(x0, offset, comm, nd, nc)
+        ts, tdg = cp.max([ts, tdg])
+        legs[name] = {"n_discard": nd, "n_collect": nc, "sampling_s": float(ts), "diag_s": float(tdg),
+                      "ess_mean": fin(np.mean(es)), "ess_min": fin(np.min(es)),
+                      "ess_per_sec_sampling": fin(np.mean(es) / ts),
+                      "ess_min_per_sec_sampling": fin(np.min(es) / ts),
+                      "ess_per_sec_end_to_end": fin(np.mean(es) / (ts + tdg)),
+                      "rhat": rhat_block(rh)}
+    comm_info = comm.info() if comm is not None else None
 
-    # PMC-derived figures of this exact launch shape (profiles/, from the
-    # rocprofv3 passes of tools/profile_bench.sh and tools/pmc_sq.sh)
-    key = f"C{C_loc}_D{D}_L{L}_K{a.steps}_{a.dtype}"
-
-    def pmc(name):
-        path = os.path.join(ROOT, "profiles", name)
-        try:
-            return json.load(open(path)).get(key) if os.path.exists(path) else None
-        except Exception:
-            return None
-
-    tr = pmc("pmc_traffic.json")
-    traffic = tr["hbm_bytes_per_launch"] if tr else None
-    vi = pmc("pmc_valu.json")
-    valu_issue = None if not vi else {
-        "frac": vi["issue_frac"], "frac_at_2p4ghz": vi["issue_frac_at_2p4ghz"],
-        "valu_insts_per_wave": vi["valu_insts_per_wave"], "clock_ghz": vi["clock_ghz"],
-        "note": "SQ_INSTS_VALU x 2 cycles (wave64 on SIMD-32) / (1024 SIMDs x kernel cycles)"}
-
-    copy_gbs = copy_ceiling(lib) if rank == 0 else None
-    ns = north_star_check(gm, a, dtype) if rank == 0 and world == 1 and a.north_star else None
-    host_out = host_output_rate(lib, sampler, a) if rank == 0 and world == 1 else None
-    per_lf = per_leapfrog_hbm(a, dtype) if rank == 0 and world == 1 else None
-
-    cpu = None
-    if rank == 0 and world == 1 and a.cpu_seconds > 0:
-        cpu = cpu_baseline(gm, a, dtype, x0, lanes, elems)
-
+    # rank-0-only measurements; the other ranks wait at the closing barrier
+    extra = {}
     if rank == 0:
+        extra["copy_ceiling_gbs"] = be.copy_ceiling()
+        extra["per_leapfrog_hbm"] = be.per_leapfrog_hbm()
+        extra["host_output"] = be.host_output(sampler)
+        extra["north_star_check"] = be.north_star_check() if a.north_star else None
+        extra["cpu_baseline"] = be.cpu_baseline(x0, lanes, elems) if a.cpu_seconds > 0 else None
+    cp.barrier()
+
+    line = None
+    if rank == 0:
+        value = C_glob * L * a.steps / t_max
+        steps_per_launch = a.steps / max(launches, 1)
+        fa = f_alg_rosenbrock(D)
+        achieved_tf = fa * C_loc * L * steps_per_launch / (launch_ms * 1e-3) / 1e12
+        hbm_bytes = b_step(D, L, s_bytes) * C_loc * steps_per_launch
+        hbm_gbs = hbm_bytes / (launch_ms * 1e-3) / 1e9
+        traffic, issue = load_pmc(C_loc, D, L, a.dtype, a.steps)
         line = {
-            "metric": "leapfrog steps/sec (whole node) + ESS/sec, 64-dim Rosenbrock HMC at 1/2/4/8 GPUs",
+            "metric": METRIC,
             "value": value,
             "unit": "chain-leapfrog steps/s",
             "n_gpus": world,
@@ -161,160 +447,48 @@ def main():
                                    f"eps={a.eps}, n_leapfrog={L}, all {a.steps} transitions collected",
                        "chains_per_gpu": C_loc, "dim": D, "n_leapfrog": L, "step_size": a.eps,
                        "layout": f"{lanes}x{elems}", "parallelism": f"chains sharded x{world}"},
-            "ess_per_sec": fin(np.mean(ess) / t_max),
-            "ess_min_per_sec": fin(np.min(ess) / t_max),
-            "ess": {"min": fin(np.min(ess)), "mean": fin(np.mean(ess))},
-            "rhat": {"min": fin(np.min(rhat)), "max": fin(np.max(rhat))},
-            "diag_seconds": t_diag,
-            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+            "timing": {"wall_ms": t_max * 1e3, "kernel_ms": kmax, "launches": launches,
+                       "host_overhead_ms": t_max * 1e3 - kmax, "per_rank": ranks,
+                       "note": "wall = barrier-bracketed timed region (max over ranks); kernel = HIP events "
+                               "around the run's launches on the sampler's stream; host_overhead = wall - kernel"},
+            "ess_per_sec": legs.get("cfg2_schedule", {}).get("ess_per_sec_sampling"),
+            "ess": legs,
+            "timed_draws_diagnostics": {"ess_mean": fin(np.mean(ess)), "ess_min": fin(np.min(ess)),
+                                        "rhat": rhat_block(rhat), "diag_s": t_diag,
+                                        "note": "the --steps draws of the timed region, started "
+                                                "--warmup transitions from N(0,1): not a mixing figure"},
+            "roofline": {"bound": "valu", "achieved": achieved_tf, "peak": VALU_F32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved_tf / VALU_F32_PEAK_TFLOPS,
+                         "traffic": traffic["bytes"] if traffic else None,
                          "kernel": "hmc_kernel", "launch_ms": launch_ms,
-                         "note": "achieved = SURVEY 8(d) algorithmic bytes (q, p, g round-trip HBM every "
-                                 "leapfrog) / launch time; the fused kernel keeps the state in VGPRs "
-                                 "(traffic = the PMC bytes it moves, mostly the collected samples), so "
-                                 "frac > 1; its real bound is VALU issue (valu); the HBM-bound "
-                                 "per-leapfrog formulation is per_leapfrog_hbm",
-                         "algorithmic_bytes_per_launch": bytes_per_launch,
-                         "valu": {"achieved_tflops": achieved_tflops,
-                                  "peak_tflops": VALU_F32_PEAK_TFLOPS,
-                                  "frac": achieved_tflops / VALU_F32_PEAK_TFLOPS,
-                                  "issue": valu_issue},
-                         "copy_ceiling_gbs": copy_gbs,
-                         "per_leapfrog_hbm": per_lf},
-            "cpu_baseline": cpu,
-            "north_star_check": ns,
-            "host_output": host_out,
+                         "flops_per_chain_leapfrog": fa,
+                         "algorithmic_flops_per_launch": fa * C_loc * L * steps_per_launch,
+                         "note": "achieved = F_alg (15(D-1)+6D per chain-leapfrog, SURVEY 8(d)) x chain-"
+                                 "leapfrogs per launch / the launch's HIP-event time; the fused kernel keeps "
+                                 "q, p, g in VGPRs, so VALU issue, not HBM, bounds it (traffic = PMC HBM bytes "
+                                 "of the launch: the collected samples plus one state read/write)",
+                         "traffic_source": traffic,
+                         "valu_issue": issue,
+                         "hbm_equivalent": {"achieved_gbs": hbm_gbs, "peak_gbs": HBM_PEAK_GBS,
+                                            "hbm_equivalent_frac": hbm_gbs / HBM_PEAK_GBS,
+                                            "algorithmic_bytes_per_launch": hbm_bytes,
+                                            "note": "BASELINE.md's per-leapfrog algorithmic bytes (q, p, g "
+                                                    "round-trip HBM every leapfrog) over the fused launch's "
+                                                    "time: a comparison with the unfused design, not a "
+                                                    "roofline fraction"},
+                         "copy_ceiling_gbs": extra.get("copy_ceiling_gbs"),
+                         "per_leapfrog_hbm": extra.get("per_leapfrog_hbm")},
+            "cpu_baseline": extra.get("cpu_baseline"),
+            "rccl": comm_info,
+            "north_star_check": extra.get("north_star_check"),
+            "host_output": extra.get("host_output"),
         }
         print(json.dumps(line), flush=True)
     if comm is not None:
         comm.close()
     sampler.close()
     cp.close()
-
-
-def per_leapfrog_hbm(a, dtype, chains=1 << 20, reps=20):
-    """The unfused, per-leapfrog design the HBM roofline is written for
-    (SURVEY.md §8(d)): gm_bv_leapfrog, one kernel per leapfrog with q, p, g
-    and logp in HBM, at an HBM-resident size (2^20 chains: 256 MiB per
-    array); achieved = B_alg (6D+1)*s per chain-leapfrog x chains / time."""
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    try:
-        from hbm_leapfrog import measure
-        r = measure(chains, a.dim, dtype, reps)
-    except Exception as e:  # reported, never fatal to the bench line
-        return {"error": str(e)}
-    return {"kernel": "leapfrog_hbm_kernel", "chains": chains, "achieved": r["achieved_gbs"],
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": r["hbm_frac"], "us_per_leapfrog": r["us_per_leapfrog"],
-            "chain_leapfrogs_per_s": r["chain_leapfrogs_per_s"]}
-
-
-def host_output_rate(lib, sampler, a):
-    """The same transitions through gm_run (HMC::run, hmc.rs:164-181): the
-    [C, N, D] sample returned in a host array (device transpose + D2H into
-    pageable memory). The PCIe-inclusive rate; never `value`."""
-    from general_mcmc_amd import _lib
-    sampler.run(a.steps, 0)  # warm (host array, staging buffers)
-    _lib.check(lib.gm_device_synchronize())
-    t0 = time.perf_counter()
-    out = sampler.run(a.steps, 0)
-    t = time.perf_counter() - t0
-    C, N, D = out.shape
-    return {"chain_leapfrogs_per_s": C * a.leapfrog * N / t, "seconds": t,
-            "sample_bytes": int(out.nbytes), "d2h_gbs_incl_sampling": out.nbytes / t / 1e9}
-
-
-def north_star_check(gm, a, dtype, chains=16384):
-    """BASELINE.json north_star's target shape: >= 10^4 chains of 64-D
-    Rosenbrock HMC on one GPU (same eps, L and collection as the bench; device
-    time of one launch). Reported beside the headline, never as `value`."""
-    D, L, n = a.dim, a.leapfrog, 100
-    s = gm.HMC(gm.RosenbrockND(), gm.init_with_seed(chains, D, 43, np.float64).astype(dtype),
-               a.eps, L, dtype=dtype).set_seed(43)
-    try:
-        s.reserve(n)
-        s.run_positions(0, 20)
-        s.run_positions(n, 0)
-        ms, launches = s.last_run_stats()
-    finally:
-        s.close()
-    sb = np.dtype(dtype).itemsize
-    b_step = (L * (6 * D + 1) + (4 * D + 2) + D) * sb
-    gbs = b_step * chains * n / (ms * 1e-3) / 1e9
-    return {"chains": chains, "chain_leapfrogs_per_s": chains * L * n / (ms * 1e-3),
-            "launch_ms": ms / max(launches, 1), "hbm_equiv_gbs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS,
-            "target": ">= 1e4 chains at >= 50% of the HBM-read roofline (BASELINE.json north_star)"}
-
-
-def fin(v):
-    """float, or None where undefined (diagnostics need >= 4 draws): keeps the
-    JSON line strict."""
-    v = float(v)
-    return v if np.isfinite(v) else None
-
-
-def copy_ceiling(lib, nbytes=1 << 30, reps=5):
-    """Empirical HBM ceiling on this box: a 1 GiB
-    device-to-device copy, read + write bytes over the median time."""
-    import ctypes as C
-    from general_mcmc_amd import _lib
-    src, dst = C.c_void_p(), C.c_void_p()
-    try:
-        _lib.check(lib.gm_malloc(C.byref(src), nbytes))
-        _lib.check(lib.gm_malloc(C.byref(dst), nbytes))
-        ts = []
-        for _ in range(reps + 1):
-            _lib.check(lib.gm_device_synchronize())
-            t0 = time.perf_counter()
-            _lib.check(lib.gm_memcpy_dtod(dst, src, nbytes))
-            _lib.check(lib.gm_device_synchronize())
-            ts.append(time.perf_counter() - t0)
-        return 2 * nbytes / float(np.median(ts[1:])) / 1e9
-    except Exception:
-        return None
-    finally:
-        for p in (src, dst):
-            if p.value:
-                lib.gm_free(p)
-
-
-def _cpu_model():
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return None
-
-
-def cpu_baseline(gm, a, dtype, x0, lanes, elems):
-    """The CPU oracle (plain-C restatement of batched_hmc.rs, multithreaded over
-    chains like the reference's rayon par_iter) timed on a bounded sample of the
-    same workload: all chains, a few transitions."""
-    from tests import _oracle
-    ora = _oracle.load()
-    threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-    t = _oracle.Target(1, a.dim, a=1.0, b=100.0)
-    q = np.array(x0, copy=True)
-    t0 = time.perf_counter()
-    ora.hmc_run(t, q, a.eps, a.leapfrog, 42, 0, 1, 1, lanes, elems, threads=threads)
-    one = time.perf_counter() - t0
-    steps = max(1, int(a.cpu_seconds / max(one, 1e-6)))
-    t0 = time.perf_counter()
-    ora.hmc_run(t, q, a.eps, a.leapfrog, 42, 1, steps, steps, lanes, elems, threads=threads)
-    dt = time.perf_counter() - t0
-    # one thread on a slice of the chains (the reference's per-core rate)
-    n1 = max(1, x0.shape[0] // threads)
-    q1 = np.array(x0[:n1], copy=True)
-    t0 = time.perf_counter()
-    ora.hmc_run(t, q1, a.eps, a.leapfrog, 42, 1, steps, steps, lanes, elems, threads=1)
-    dt1 = time.perf_counter() - t0
-    return {"value": x0.shape[0] * a.leapfrog * steps / dt, "unit": "chain-leapfrog steps/s",
-            "cores": threads, "kind": "port",
-            "sample": f"{x0.shape[0]} chains x {steps} transitions x {a.leapfrog} leapfrogs "
-                      f"(oracle/gm_oracle.c, {threads} threads, {dt:.1f}s)",
-            "one_thread_value": n1 * a.leapfrog * steps / dt1,
-            "host": {"cpu_model": _cpu_model(), "nproc": os.cpu_count()}}
+    return line
 
 
 if __name__ == "__main__":

@@ -91,6 +91,7 @@ SIGNATURES = {
     "gm_sampler_set_layout": (_ip, [_vp, _i32, _i32]),
     "gm_sampler_last_run_stats": (_ip, [_vp, C.POINTER(_dbl), C.POINTER(_i64)]),
     "gm_sampler_set_steps_per_launch": (_ip, [_vp, _i64]),
+    "gm_sampler_set_chains_per_wave": (_ip, [_vp, _i32]),
     "gm_sampler_reserve": (_ip, [_vp, _i64]),
     "gm_state_size": (_ip, [_vp, C.POINTER(_u64)]),
     "gm_state_save": (_ip, [_vp, _vp, _u64]),
@@ -101,6 +102,7 @@ SIGNATURES = {
     "gm_comm_get_unique_id": (_ip, [_vp]),
     "gm_comm_init": (_ip, [_vp, _i32, _i32, C.POINTER(_vp)]),
     "gm_comm_destroy": (_ip, [_vp]),
+    "gm_comm_info": (_ip, [_vp, C.POINTER(_i32), C.POINTER(_i32), C.POINTER(_i32)]),
     "gm_split_rhat_ess_dist": (_ip, [_vp, _vp, _ip, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
     "gm_split_rhat_ess_shards": (_ip, [_vp, _ip, _ip, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _vp]),
     # run_progress statistics

@@ -152,6 +152,7 @@ struct gm_sampler {
   size_t zs_bytes = 0;
   Layout lay;
   long long steps_per_launch = 1000;
+  int chains_per_wave = 0;  // HMC 64-lane layouts: 0 automatic, 1 or 2
   std::vector<hipEvent_t> evs;
   double last_ms = 0;
   long long last_launches = 0;
@@ -561,6 +562,13 @@ int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems) {
   return GM_OK;
 }
 
+int gm_sampler_set_chains_per_wave(gm_sampler* s, int32_t chains_per_wave) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(chains_per_wave >= 0 && chains_per_wave <= 2, "chains_per_wave must be 0 (automatic), 1 or 2");
+  s->chains_per_wave = chains_per_wave;
+  return GM_OK;
+}
+
 int gm_sampler_set_steps_per_launch(gm_sampler* s, int64_t steps) {
   GM_REQ(s, "sampler is NULL");
   // the kernels take a launch's transition count as an int
@@ -583,16 +591,11 @@ int gm_sampler_last_run_stats(gm_sampler* s, double* kernel_ms, int64_t* launche
   return GM_OK;
 }
 
-// Runs `total` transitions; transitions with index >= collect_from (0-based
-// within this call) are stored at sample rows (index - collect_from).
-// Leapfrog-loop unroll of the HMC kernel (a tuning knob with identical
-// results; GM_HMC_UNROLL=1|4 overrides the default for measurements).
-// Measured (tools/probe_hmc_scaling.py, PROBE_UNROLLS=1,4): x4 is ~12%
-// faster while the grid has at most one wave per SIMD (latency bound), and
-// 10-20% slower from two waves per SIMD up.
+// Leapfrog-loop unroll of the HMC kernel (identical results). Measured
+// (tools/probe_hmc_scaling.py): x4 is ~12% faster while the grid has at most
+// one wave per SIMD (latency bound), and 10-20% slower from two waves per
+// SIMD up.
 static int hmc_lf_unroll(long long waves) {
-  const char* v = getenv("GM_HMC_UNROLL");
-  if (v) return atoi(v) == 4 ? 4 : 1;
   static const int simds = [] {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -603,10 +606,41 @@ static int hmc_lf_unroll(long long waves) {
   return waves <= simds ? 4 : 1;
 }
 
+// Chains per wave of the 64-lane HMC kernel (automatic choice; identical
+// results either way): see hmc_kernel_cw.
+static int hmc_chains_per_wave(const gm_sampler* s) {
+  (void)s;
+  return 1;
+}
+
+// hipSetDevice only when the calling thread is on another device (the call
+// is on every run's path)
+static hipError_t use_device(int dev) {
+  static thread_local int cur = -1;
+  if (cur == dev) return hipSuccess;
+  const hipError_t e = hipSetDevice(dev);
+  if (e == hipSuccess) cur = dev;
+  return e;
+}
+
+// One event pair per run (before the first launch, after the last): the
+// device time of the run's launches, read back after the run's stream
+// synchronize.
+static int ensure_run_events(gm_sampler* s) {
+  while (s->evs.size() < 2) {
+    hipEvent_t ev;
+    GM_HIP(hipEventCreate(&ev));
+    s->evs.push_back(ev);
+  }
+  return GM_OK;
+}
+
+// Runs `total` transitions; transitions with index >= collect_from (0-based
+// within this call) are stored at sample rows (index - collect_from).
 static int run_steps(gm_sampler* s, long long total, long long collect_from, int progress,
                      const TrackLaunch* trk = nullptr, const StepHook* hook = nullptr,
                      long long chunk_override = 0) {
-  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(use_device(s->device));
   s->last_ms = 0;
   s->last_launches = 0;
   // NUTS always launches: init_chain_state + row 0 even with zero transitions
@@ -620,20 +654,17 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
   }
   const long long chunk = chunk_override > 0 ? chunk_override : s->steps_per_launch;
   const long long n_launch = (total + chunk - 1) / chunk;
-  while ((long long)s->evs.size() < 2 * n_launch) {
-    hipEvent_t ev;
-    GM_HIP(hipEventCreate(&ev));
-    s->evs.push_back(ev);
-  }
-  long long li = 0;
-  for (long long start = 0; start < total; start += chunk, ++li) {
+  int rc = ensure_run_events(s);
+  if (rc) return rc;
+  const int lf_unroll = s->kind == K_HMC ? hmc_lf_unroll((s->C * s->lay.lanes + 63) / 64) : 1;
+  GM_HIP(hipEventRecord(s->evs[0], s->stream));
+  for (long long start = 0; start < total; start += chunk) {
     const long long n = total - start < chunk ? total - start : chunk;
     long long cf = collect_from - start;
     if (cf < 0) cf = 0;
     if (cf > n) cf = n;
     long long row0 = start - collect_from;
     if (row0 < 0) row0 = 0;
-    GM_HIP(hipEventRecord(s->evs[2 * li], s->stream));
     hipError_t e;
     if (s->kind == K_HMC) {
       HmcLaunch a;
@@ -651,14 +682,14 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
       a.n_steps = (int)n;
       a.collect_from = (int)cf;
       a.sample_row0 = row0;
-      a.lf_unroll = hmc_lf_unroll((s->C * s->lay.lanes + 63) / 64);
-      {
-        const char* v = getenv("GM_HMC_STAGGER");  // measurement knob
-        a.stagger = v ? (atoi(v) != 0) : 1;
-      }
+      a.lf_unroll = lf_unroll;
+      a.chains_per_wave = s->chains_per_wave ? s->chains_per_wave : hmc_chains_per_wave(s);
+#ifdef GM_AB_CW
+      a.chains_per_wave = GM_AB_CW;  // A/B builds only
+#endif
       if (layout_is_wide(s->lay)) {
         const size_t need = (size_t)s->C * (s->dt == GM_F32 ? 4 : 2) * s->lay.lanes * s->lay.elems * s->esz;
-        int rc = ensure_buf(&s->d_zs, &s->zs_bytes, need);
+        rc = ensure_buf(&s->d_zs, &s->zs_bytes, need);
         if (rc) return rc;
         a.zs = s->d_zs;
       }
@@ -688,22 +719,18 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
       set_error(std::string("kernel launch failed: ") + hipGetErrorString(e));
       return GM_EHIP;
     }
-    GM_HIP(hipEventRecord(s->evs[2 * li + 1], s->stream));
     if (hook && *hook) {
-      const int rc = (*hook)(start + n);
+      rc = (*hook)(start + n);
       if (rc) return rc;
     }
   }
+  GM_HIP(hipEventRecord(s->evs[1], s->stream));
   s->step += total;
   s->total_steps += total;
   GM_HIP(hipStreamSynchronize(s->stream));
-  double ms = 0;
-  for (long long i = 0; i < n_launch; ++i) {
-    float t = 0;
-    GM_HIP(hipEventElapsedTime(&t, s->evs[2 * i], s->evs[2 * i + 1]));
-    ms += t;
-  }
-  s->last_ms = ms;
+  float t = 0;
+  GM_HIP(hipEventElapsedTime(&t, s->evs[0], s->evs[1]));
+  s->last_ms = t;
   s->last_launches = n_launch;
   return GM_OK;
 }
@@ -712,7 +739,7 @@ static int run_impl(gm_sampler* s, int64_t n_collect, int64_t n_discard, int pro
   GM_REQ(s, "sampler is NULL");
   s->last_rows = n_collect;
   GM_REQ(n_collect >= 0 && n_discard >= 0, "n_collect and n_discard must be >= 0");
-  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(use_device(s->device));
   int rc = ensure_buf(&s->d_samples, &s->samples_bytes, (size_t)n_collect * s->C * s->D * s->esz);
   if (rc) return rc;
   long long total = n_discard + n_collect;

@@ -4,8 +4,10 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <array>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -79,6 +81,8 @@ struct gm_comm {
   int rank = 0;
   int device = 0;
   hipStream_t stream = nullptr;
+  // shapes (C, N, P, dtype) already checked equal on every rank
+  std::set<std::array<long long, 4>> checked;
 };
 
 static int local_diag(const void* dev_sample, gm_dtype dtype, int64_t C, int64_t N, int64_t P,
@@ -103,20 +107,27 @@ static int local_diag(const void* dev_sample, gm_dtype dtype, int64_t C, int64_t
   if (rc) return rc;
   const double *pcm = (double*)cm.p, *ps2 = (double*)s2.p, *pac = (double*)ac.p;
   if (R > 1) {
-    // all ranks must hold equally many chains (contiguous equal shards)
-    DevBuf &cnt = B.cnt, &cnt_all = B.cnt_all;
-    if ((rc = cnt.alloc(sizeof(long long))) || (rc = cnt_all.alloc(sizeof(long long) * R))) return rc;
-    long long c64 = C;
-    GM_HIP(hipMemcpyAsync(cnt.p, &c64, sizeof(long long), hipMemcpyHostToDevice, st));
-    GM_NCCL(ncclAllGather(cnt.p, cnt_all.p, 1, ncclInt64, comm->comm, st));
-    std::vector<long long> counts(R);
-    GM_HIP(hipMemcpyAsync(counts.data(), cnt_all.p, sizeof(long long) * R, hipMemcpyDeviceToHost, st));
-    GM_HIP(hipStreamSynchronize(st));
-    for (int r = 0; r < R; ++r)
-      if (counts[r] != C) {
-        set_error("gm_split_rhat_ess_dist: all ranks must hold the same number of chains");
-        return GM_EINVAL;
-      }
+    // Every rank must pass the same shape: the grouped all-gather below is
+    // sized from it, and unequal sizes would not match up across ranks. A
+    // shape is checked once per communicator (one 4-word all-gather + host
+    // sync), then trusted: the ranks call in lockstep with equal shapes, so
+    // they all take the same branch here.
+    const std::array<long long, 4> shape{(long long)C, (long long)N, (long long)P, (long long)dtype};
+    if (!comm->checked.count(shape)) {
+      DevBuf &cnt = B.cnt, &cnt_all = B.cnt_all;
+      if ((rc = cnt.alloc(sizeof(shape))) || (rc = cnt_all.alloc(sizeof(shape) * R))) return rc;
+      GM_HIP(hipMemcpyAsync(cnt.p, shape.data(), sizeof(shape), hipMemcpyHostToDevice, st));
+      GM_NCCL(ncclAllGather(cnt.p, cnt_all.p, 4, ncclInt64, comm->comm, st));
+      std::vector<std::array<long long, 4>> all(R);
+      GM_HIP(hipMemcpyAsync(all.data(), cnt_all.p, sizeof(shape) * R, hipMemcpyDeviceToHost, st));
+      GM_HIP(hipStreamSynchronize(st));
+      for (int r = 0; r < R; ++r)
+        if (all[r] != shape) {
+          set_error("gm_split_rhat_ess_dist: all ranks must pass the same chain count, draws, params and dtype");
+          return GM_EINVAL;
+        }
+      comm->checked.insert(shape);
+    }
     if ((rc = cm_all.alloc(sizeof(double) * 2 * C * P * R)) ||
         (rc = s2_all.alloc(sizeof(double) * 2 * C * P * R)) ||
         (rc = ac_all.alloc(sizeof(double) * h * P * R)))
@@ -220,6 +231,18 @@ int gm_comm_destroy(gm_comm* comm) {
   if (comm->comm) ncclCommDestroy(comm->comm);
   if (comm->stream) hipStreamDestroy(comm->stream);
   delete comm;
+  return GM_OK;
+}
+
+int gm_comm_info(gm_comm* comm, int32_t* nranks, int32_t* rank, int32_t* device) {
+  GM_REQ(comm && comm->comm, "comm is NULL");
+  int n = 0, r = 0, d = 0;
+  GM_NCCL(ncclCommCount(comm->comm, &n));
+  GM_NCCL(ncclCommUserRank(comm->comm, &r));
+  GM_NCCL(ncclCommCuDevice(comm->comm, &d));
+  if (nranks) *nranks = n;
+  if (rank) *rank = r;
+  if (device) *device = d;
   return GM_OK;
 }
 

@@ -16,7 +16,6 @@
 // The gradient at the current point is carried across transitions (the
 // reference re-evaluates it twice per step, batched_hmc.rs:138,169; same
 // values), so a transition costs exactly L target evaluations.
-#include <stdlib.h>
 #include "hmc_device.h"
 #include "gm_jit.h"
 #include "gm_layouts.h"
@@ -37,10 +36,20 @@ hipError_t launch_hmc(gm_dtype dt, const TargetDev& tg, const Layout& lay, const
     });
   }
   return dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
+    const size_t lds = t.template lds_bytes<LPC, E>();
+    if constexpr (LPC == 64) {
+      using TL = decltype(t.template bind<LPC, E>(0));
+      if constexpr (requires { TL::template has_part<LPC>; }) {
+        if (a.chains_per_wave == 2) {  // two chains per wave (hmc_kernel_cw)
+          const long long threads = (a.C + 1) / 2 * 64;
+          const unsigned blocks = (unsigned)((threads + 255) / 256);
+          hipLaunchKernelGGL((hmc_kernel_cw<T, E, 2, TG>), dim3(blocks), dim3(256), lds, st, a, t);
+          return hipGetLastError();
+        }
+      }
+    }
     const long long threads = a.C * LPC;
     const unsigned blocks = (unsigned)((threads + 255) / 256);
-    size_t lds = t.template lds_bytes<LPC, E>();
-    if (const char* v = getenv("GM_HMC_LDS_PAD")) lds += (size_t)atol(v);  // measurement knob
     hipLaunchKernelGGL((hmc_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), lds, st, a, t);
     return hipGetLastError();
   });

@@ -53,6 +53,14 @@ class ControlPlane:
         self.dist.broadcast_object_list(obj, src=src)
         return obj[0]
 
+    def gather(self, obj) -> list:
+        """Every rank's obj, on every rank (rank order)."""
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
     def max(self, values) -> np.ndarray:
         v = np.asarray(values, dtype=np.float64)
         if self.dist is None:
@@ -84,6 +92,13 @@ class Comm:
         h = C.c_void_p()
         _lib.check(self.lib.gm_comm_init(buf, cp.world, cp.rank, C.byref(h)))
         self.h = h
+
+    def info(self) -> dict:
+        """What RCCL reports for this communicator (ncclCommCount /
+        ncclCommUserRank / ncclCommCuDevice)."""
+        n, r, d = C.c_int32(), C.c_int32(), C.c_int32()
+        _lib.check(self.lib.gm_comm_info(self.h, C.byref(n), C.byref(r), C.byref(d)))
+        return {"nranks": n.value, "rank": r.value, "device": d.value}
 
     def split_rhat_ess(self, ds) -> tuple[np.ndarray, np.ndarray]:
         """Diagnostics of the union of all ranks' chains from each rank's

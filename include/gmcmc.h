@@ -226,6 +226,12 @@ int gm_nuts_get_mass(gm_sampler* s, int32_t* mode, int32_t* kind, void* dinv, vo
 int gm_sampler_layout(gm_sampler* s, int32_t* lanes, int32_t* elems);
 int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems);
 
+/* HMC with a 64-lane layout (lanes == 64): chains sharing one wavefront,
+ * each lane holding the same coordinates of each (0 = automatic, 1, 2). Two
+ * chains per wave issue two independent instruction streams per wave (more
+ * latency hidden at low occupancy); samples are bit-identical either way. */
+int gm_sampler_set_chains_per_wave(gm_sampler* s, int32_t chains_per_wave);
+
 /* Device time (ms) of the sampling kernels launched by the last run, and the
  * number of launches (HIP events on the sampler's stream). */
 int gm_sampler_last_run_stats(gm_sampler* s, double* kernel_ms, int64_t* launches);
@@ -276,8 +282,16 @@ typedef struct gm_comm gm_comm;
 int gm_comm_get_unique_id(void* id_out /* GM_UNIQUE_ID_BYTES */);
 int gm_comm_init(const void* id, int32_t nranks, int32_t rank, gm_comm** out);
 int gm_comm_destroy(gm_comm* comm);
+/* What RCCL itself reports for the communicator (ncclCommCount,
+ * ncclCommUserRank, ncclCommCuDevice): the ranks the exchange really spans.
+ * Any pointer may be NULL. */
+int gm_comm_info(gm_comm* comm, int32_t* nranks, int32_t* rank, int32_t* device);
 /* Same result on every rank: diagnostics of the union of all ranks' chains
- * (rank r holds global chains [offset_r, offset_r + n_chains_local)). */
+ * (rank r holds global chains [offset_r, offset_r + n_chains_local)).
+ * Every rank must pass the same (n_chains_local, n_draws, n_params, dtype).
+ * The first call with a given shape on a communicator checks that with one
+ * small all-gather (a mismatch is GM_EINVAL on every rank); later calls with
+ * that shape go straight to the one grouped all-gather of the summaries. */
 int gm_split_rhat_ess_dist(gm_comm* comm, const void* dev_sample, gm_dtype dtype,
                            int64_t n_chains_local, int64_t n_draws, int64_t n_params,
                            int64_t stride_chain, int64_t stride_draw, int64_t stride_param,

@@ -88,6 +88,34 @@ def load():
     return Oracle(lib)
 
 
+class CpuHmc:
+    """oracle/libcpu_hmc.so: bench.py's CPU baseline (the reference's batched
+    HMC op structure at -O3; not bit-matching -- see cpu_hmc.c)."""
+
+    def __init__(self, lib):
+        self.lib = lib
+        lib.cpu_hmc_rosenbrock_f32.argtypes = [_vp, _i64, _int, _dbl, _int, _i64, _u64, _int, _vp]
+
+    def run(self, q, eps, L, n_steps, seed, threads, accepts=None):
+        assert q.dtype == np.float32 and q.flags["C_CONTIGUOUS"]
+        rc = self.lib.cpu_hmc_rosenbrock_f32(_p(q), q.shape[0], q.shape[1], eps, L, n_steps, seed, threads,
+                                             _p(accepts))
+        assert rc == 0
+
+
+def cpu_hmc():
+    """The CPU-baseline library, or None if it is not built."""
+    path = os.path.join(ORACLE_DIR, "libcpu_hmc.so")
+    if not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(os.path.join(ORACLE_DIR, "cpu_hmc.c")):
+        try:
+            build()
+        except Exception:
+            return None
+    if not os.path.exists(path):
+        return None
+    return CpuHmc(C.CDLL(path))
+
+
 class or_mass_cfg(C.Structure):
     _fields_ = [("mode", C.c_int), ("start_buffer", C.c_int64), ("end_buffer", C.c_int64),
                 ("initial_window", C.c_int64), ("regularize", C.c_double), ("jitter", C.c_double)]

@@ -1,0 +1,151 @@
+"""bench.py's aggregation and JSON assembly, run on the CPU with the GPU calls
+stubbed (the GpuBench class replaced): at world_size 2 under gloo -- the path
+that produces the driver's multi-GPU SCALE lines -- rank 0 must emit every
+field of the world_size 1 line, take the max over ranks, and carry each rank's
+timing, the communicator's rank count and the CPU baseline."""
+import json
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGV = ["--steps", "8", "--warmup", "2", "--chains", "128", "--cpu-seconds", "0.05",
+        "--ess-discard", "4", "--ess-collect", "8", "--ess-long-discard", "4", "--ess-long-collect", "8"]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _Samples:
+    def __init__(self, n, c, d):
+        self.n_collect, self.n_chains, self.dim = n, c, d
+
+
+class _Sampler:
+    def __init__(self, x0, rank):
+        self.C, self.D, self.rank = x0.shape[0], x0.shape[1], rank
+
+    def layout(self):
+        return 64, 1
+
+    def reserve(self, n):
+        return self
+
+    def run_positions(self, n, nd):
+        return _Samples(n, self.C, self.D)
+
+    def last_run_stats(self):  # rank 1 is the slower one
+        return (2.0 if self.rank == 1 else 1.0), 1
+
+    def close(self):
+        pass
+
+
+class _Comm:
+    def __init__(self, cp):
+        self.cp = cp
+
+    def info(self):
+        return {"nranks": self.cp.world, "rank": self.cp.rank, "device": self.cp.local_rank}
+
+    def close(self):
+        pass
+
+
+def stub_backend():
+    import bench
+
+    class StubBench:
+        def __init__(self, a, cp):
+            self.a, self.cp = a, cp
+
+        def init_positions(self, n, offset, count):
+            return np.random.default_rng(offset).standard_normal((count, self.a.dim)).astype(np.float32)
+
+        def sampler(self, x0, offset):
+            return _Sampler(x0, self.cp.rank)
+
+        def sync(self):
+            pass
+
+        def comm(self):
+            return _Comm(self.cp) if self.cp.world > 1 else None
+
+        def diagnostics(self, ds, comm):
+            return np.full(ds.dim, 0.99, np.float32), np.full(ds.dim, 100.0 * ds.n_chains, np.float32)
+
+        def ess_leg(self, x0, offset, comm, nd, nc):
+            r, e = self.diagnostics(_Samples(nc, x0.shape[0], x0.shape[1]), comm)
+            return 0.01 * (1 + self.cp.rank), 0.001, r, e
+
+        def copy_ceiling(self):
+            return 5000.0
+
+        def per_leapfrog_hbm(self):
+            return {"achieved": 5000.0, "frac": 0.625}
+
+        def host_output(self, sampler):
+            return {"chain_leapfrogs_per_s": 1.0}
+
+        def north_star_check(self):
+            return None
+
+        def cpu_baseline(self, x0, lanes, elems):
+            return bench.cpu_baseline(self.a, np.float32, x0, lanes, elems)
+
+    return StubBench
+
+
+def _worker(rank, world, port, outdir):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    import bench
+    line = bench.main(ARGV + ["--gpus", str(world)], backend=stub_backend())
+    if rank == 0:
+        with open(os.path.join(outdir, f"line{world}.json"), "w") as f:
+            json.dump(line, f)
+    else:
+        assert line is None
+
+
+def _keys(d, prefix=""):
+    out = set()
+    for k, v in d.items():
+        out.add(prefix + k)
+        if isinstance(v, dict) and k not in ("ess", "per_rank"):
+            out |= _keys(v, prefix + k + ".")
+    return out
+
+
+def test_bench_line_world1_and_world2(tmp_path):
+    for world in (1, 2):
+        mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                           start_method="spawn", join=True)
+    l1 = json.load(open(tmp_path / "line1.json"))
+    l2 = json.load(open(tmp_path / "line2.json"))
+    # the N = 2 line carries every field of the N = 1 line
+    missing = _keys(l1) - _keys(l2)
+    assert not missing, missing
+    assert l2["n_gpus"] == 2 and l1["n_gpus"] == 1
+    # whole-job value over the slowest rank's time; per-rank timing kept
+    assert len(l2["timing"]["per_rank"]) == 2
+    assert l2["roofline"]["launch_ms"] == 2.0  # the slower rank's kernel
+    assert l2["rccl"] == {"nranks": 2, "rank": 0, "device": 0}
+    assert l1["rccl"] is None
+    for line in (l1, l2):
+        assert line["roofline"]["bound"] == "valu" and 0 < line["roofline"]["frac"]
+        cb = line["cpu_baseline"]
+        assert cb["cores"] >= 1 and cb["value"] > 0 and "sched_getaffinity" in cb["host"]
+        assert set(line["ess"]) == {"cfg2_schedule", "long"}
+        assert line["ess"]["cfg2_schedule"]["rhat"]["stan_sqrt_V_over_W"]["max"] > 1.0
+    # the ESS legs time the slowest rank
+    assert l2["ess"]["cfg2_schedule"]["sampling_s"] == 0.02

@@ -159,3 +159,25 @@ def test_split_rhat_ess_matches_oracle(gm, oracle, shape, dtype):
     orr, oe = oracle.split_rhat_ess(x)
     np.testing.assert_allclose(r, orr, atol=1e-3)  # north-star tolerance: R-hat within 1e-3
     np.testing.assert_allclose(e, oe, rtol=1e-3)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("dim,lay", [(33, (64, 1)), (64, (64, 1)), (100, (64, 2)), (256, (64, 4))])
+@pytest.mark.parametrize("n_chains", [24, 25])  # an odd count leaves one wave a single chain
+def test_hmc_two_chains_per_wave_bitwise(gm, oracle, dtype, dim, lay, n_chains):
+    """hmc_kernel_cw (two chains per wavefront) == the oracle == hmc_kernel."""
+    L, eps = 7, 0.01
+    x0 = start(gm, n_chains, dim, dtype)
+    for name, t in targets(gm, dim):
+        outs = []
+        for cw in (2, 1):
+            s = gm.HMC(t, x0, eps, L, dtype=dtype).set_seed(11)
+            s.set_layout(*lay).set_chains_per_wave(cw)
+            s.set_steps_per_launch(5)
+            outs.append((s.run(6, 3), s.positions(), s.accept_counts()))
+            s.close()
+        q, samples, acc = oracle.hmc_run(Target.from_product(t, dim), x0, eps, L, 11, 0, 9, 3, *lay)
+        np.testing.assert_array_equal(outs[0][0], samples.transpose(1, 0, 2), err_msg=name)
+        np.testing.assert_array_equal(outs[0][1], q, err_msg=name)
+        np.testing.assert_array_equal(outs[0][2], acc, err_msg=name)
+        np.testing.assert_array_equal(outs[0][0], outs[1][0], err_msg=name)

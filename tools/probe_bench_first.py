@@ -1,0 +1,50 @@
+"""The bench's timed region as the driver runs it (a fresh process, W warm-up
+transitions, one timed run of K), then the same call repeated: how much of the
+first timed call's wall time is first-call cost, and what a warm-up that
+collects into the reserved sample buffer changes.
+
+    python tools/probe_bench_first.py [--warm-collect] [--steps 20 --warmup 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import general_mcmc_amd as gm  # noqa: E402
+from general_mcmc_amd import _lib  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--warmup", type=int, default=5)
+ap.add_argument("--warm-collect", action="store_true")
+ap.add_argument("--repeat", type=int, default=8)
+ap.add_argument("--cw", type=int, default=0)
+a = ap.parse_args()
+lib = _lib.load()
+_lib.check(lib.gm_set_device(0))
+lib = _lib.require_gpu()
+x0 = gm.init_with_seed(4096, 64, 42, np.float64).astype(np.float32)
+s = gm.HMC(gm.RosenbrockND(), x0, 0.01, 50).set_seed(42)
+s.set_chains_per_wave(a.cw)
+s.reserve(a.steps)
+if a.warm_collect:
+    s.run_positions(a.warmup, 0)
+else:
+    s.run_positions(0, a.warmup)
+walls, kerns = [], []
+for i in range(1 + a.repeat):
+    _lib.check(lib.gm_device_synchronize())
+    t0 = time.perf_counter()
+    s.run_positions(a.steps, 0)
+    _lib.check(lib.gm_device_synchronize())
+    walls.append((time.perf_counter() - t0) * 1e6)
+    kerns.append(s.last_run_stats()[0] * 1e3)
+print(json.dumps({"lib": os.environ.get("GMCMC_LIB", "default"), "warm_collect": a.warm_collect, "cw": a.cw,
+                  "first_wall_us": walls[0], "first_kernel_us": kerns[0],
+                  "repeat_wall_us_median": float(np.median(walls[1:])),
+                  "repeat_kernel_us_median": float(np.median(kerns[1:])),
+                  "walls": [round(w, 1) for w in walls], "kernels": [round(k, 1) for k in kerns]}))

@@ -21,16 +21,12 @@ for kind, L, C, D in cases:
     s.run_positions(0, 8)
     samplers.append((kind, L, C, D, s))
 res = {}
-knob = os.environ.get("PROBE_KNOB", "GM_HMC_UNROLL")
-unrolls = [u for u in os.environ.get("PROBE_VALUES", os.environ.get("PROBE_UNROLLS", "1")).split(",")]
 for r in range(5):
-    for u in unrolls:
-        os.environ[knob] = u
-        for kind, L, C, D, s in samplers:
-            n_steps = 400 if kind == "N400" else 40
-            s.run_positions(n_steps, 0)
-            ms, n = s.last_run_stats()
-            res.setdefault((kind, L, C, u), []).append(ms * 1e3 / n_steps)
-out = [{"kind": k[0], "L": k[1], "C": k[2], "unroll": k[3], "us_per_transition": float(np.median(v)),
+    for kind, L, C, D, s in samplers:
+        n_steps = 400 if kind == "N400" else 40
+        s.run_positions(n_steps, 0)
+        ms, n = s.last_run_stats()
+        res.setdefault((kind, L, C), []).append(ms * 1e3 / n_steps)
+out = [{"kind": k[0], "L": k[1], "C": k[2], "us_per_transition": float(np.median(v)),
         "chain_lf_per_s": k[2] * max(k[1], 1) / (np.median(v) * 1e-6)} for k, v in res.items()]
 print(json.dumps(out, indent=0))
