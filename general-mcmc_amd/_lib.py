@@ -86,12 +86,12 @@ SIGNATURES = {
     "gm_get_leapfrog_counts": (_ip, [_vp, _vp]),
     "gm_nuts_get_step_size": (_ip, [_vp, _vp, _vp]),
     "gm_nuts_set_mass_adaptation": (_ip, [_vp, _i32, _i64, _i64, _i64, _dbl, _dbl, _i64]),
+    "gm_nuts_set_lds_levels": (_ip, [_vp, _i32]),
     "gm_nuts_get_mass": (_ip, [_vp, C.POINTER(_i32), _vp, _vp, _vp, _vp, _vp]),
     "gm_sampler_layout": (_ip, [_vp, C.POINTER(_i32), C.POINTER(_i32)]),
     "gm_sampler_set_layout": (_ip, [_vp, _i32, _i32]),
     "gm_sampler_last_run_stats": (_ip, [_vp, C.POINTER(_dbl), C.POINTER(_i64)]),
     "gm_sampler_set_steps_per_launch": (_ip, [_vp, _i64]),
-    "gm_sampler_set_chains_per_wave": (_ip, [_vp, _i32]),
     "gm_sampler_reserve": (_ip, [_vp, _i64]),
     "gm_state_size": (_ip, [_vp, C.POINTER(_u64)]),
     "gm_state_save": (_ip, [_vp, _vp, _u64]),

@@ -200,12 +200,6 @@ class Sampler:
         _lib.check(self._lib.gm_sampler_reserve(self._h, n_collect))
         return self
 
-    def set_chains_per_wave(self, n: int):
-        """HMC, 64-lane layouts: chains per wavefront (0 automatic, 1, 2);
-        identical samples either way."""
-        _lib.check(self._lib.gm_sampler_set_chains_per_wave(self._h, n))
-        return self
-
     def set_steps_per_launch(self, n: int):
         _lib.check(self._lib.gm_sampler_set_steps_per_launch(self._h, n))
         return self

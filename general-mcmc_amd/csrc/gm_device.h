@@ -256,14 +256,39 @@ template <class T, int E> struct RosenbrockLane {
     if (LOGP) return -group_sum<LPC>(part);
     return (T)0;
   }
-  // The 64-lane form split for callers that reduce the log-density together
-  // with another per-chain sum (hmc_kernel's last leapfrog): eval_part
-  // returns this lane's unreduced term, logp = finish(group_sum(part)).
-  template <int LPC> static constexpr bool has_part = (LPC == 64);
+  // The evaluation split for callers that reduce the log-density together
+  // with another per-chain sum (hmc_kernel's last leapfrog, every NUTS leaf):
+  // eval_part returns this lane's unreduced term (the operations of eval),
+  // logp = finish(group_sum(part)).
+  template <int LPC> static constexpr bool has_part = true;
   template <int LPC, int E_>
   __device__ __forceinline__ T eval_part(const T (&x)[E], T (&g)[E], int) const {
-    static_assert(E_ == E && LPC == 64, "64-lane form only");
-    return eval64<true>(x, g);
+    static_assert(E_ == E, "layout mismatch");
+    if constexpr (LPC == 64) {
+      return eval64<true>(x, g);
+    } else {
+      T t[E];
+      const T nx = from_next<LPC>(x[0]);
+      const T px = from_prev<LPC>(x[E - 1]);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const T xn = (e + 1 < E) ? x[(e + 1 < E) ? e + 1 : e] : nx;
+        t[e] = xn - x[e] * x[e];
+      }
+      const T tp = x[0] - px * px;
+      T part = (T)0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const T tprev = (e > 0) ? t[(e > 0) ? e - 1 : 0] : tp;
+        const T am = a - x[e];
+        const T A = keep((b4 * x[e]) * t[e] + (T)2 * am, ms[e]);
+        const T B = keep(b2 * tprev, mp[e]);
+        g[e] = A - B;
+        const T s = keep(b * (t[e] * t[e]) + am * am, ms[e]);
+        part = (e == 0) ? s : part + s;
+      }
+      return part;
+    }
   }
   __device__ __forceinline__ T finish(T total) const { return -total; }
   template <bool LOGP>
@@ -375,6 +400,21 @@ template <class T> struct IsoGaussT {
   int D;
   template <int LPC, int E> __host__ __device__ size_t lds_bytes() const { return 0; }
   template <int LPC, int E> __device__ __forceinline__ IsoGaussT bind(int) const { return *this; }
+  // unreduced term sum x^2 of this lane; logp = finish(group_sum(part))
+  template <int LPC> static constexpr bool has_part = true;
+  template <int LPC, int E>
+  __device__ __forceinline__ T eval_part(const T (&x)[E], T (&g)[E], int lane) const {
+    T part = (T)0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      g[e] = (i < D) ? (-x[e]) / var : (T)0;
+      const T s = (i < D) ? x[e] * x[e] : (T)0;
+      part = (e == 0) ? s : part + s;
+    }
+    return part;
+  }
+  __device__ __forceinline__ T finish(T total) const { return ((T)-0.5 * total) / var; }
   template <int LPC, int E, bool LOGP>
   __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int lane) const {
     T part = (T)0;

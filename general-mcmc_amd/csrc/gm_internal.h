@@ -36,9 +36,41 @@ bool wide_layout_supported(int lanes, int elems, gm_dtype dt);
 constexpr int GM_WIDE_MAX_DIM = 16384;
 Layout default_layout(int D, gm_dtype dt, int kind);
 
+// Events a launcher records around its kernel (either may be null): the AOT
+// kernels carry them in their dispatch (hipExtLaunchKernel), so timing a run
+// adds no packets of its own to the stream.
+struct LaunchEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+
+// An AOT kernel launch carrying its timing events in the dispatch.
+template <class... A>
+hipError_t launch_timed(void (*k)(A...), dim3 grid, dim3 block, size_t lds, hipStream_t st, LaunchEvents ev,
+                        A... args) {
+#ifdef GM_AB_EVREC  // A/B builds only: separate event-record packets
+  if (ev.start) hipEventRecord(ev.start, st);
+  hipLaunchKernelGGL(k, grid, block, lds, st, args...);
+  if (ev.stop) hipEventRecord(ev.stop, st);
+  return hipGetLastError();
+#else
+  void* ptrs[] = {(void*)&args...};
+  const hipError_t e = hipExtLaunchKernel((const void*)k, grid, block, ptrs, lds, st, ev.start, ev.stop, 0);
+  return e != hipSuccess ? e : hipGetLastError();
+#endif
+}
+// The same events around a launch path that goes through another API (the
+// runtime-compiled user-target kernels).
+template <class F>
+hipError_t with_events(LaunchEvents ev, hipStream_t st, F&& launch) {
+  hipError_t e = ev.start ? hipEventRecord(ev.start, st) : hipSuccess;
+  if (e == hipSuccess) e = launch();
+  if (e == hipSuccess && ev.stop) e = hipEventRecord(ev.stop, st);
+  return e;
+}
+
 // ---- HMC -------------------------------------------------------------------
 hipError_t launch_hmc(gm_dtype dt, const TargetDev& tg, const Layout& lay, const HmcLaunch& a,
-                      hipStream_t st);
+                      hipStream_t st, LaunchEvents ev = {});
 
 // ---- run_progress statistics (gm_track.h, tracker_kernels.hip) -------------
 // ChainTracker::new for every chain from the current positions
@@ -57,7 +89,7 @@ hipError_t launch_mct_rhat(long long C, int P, unsigned long long n, const float
 
 // ---- MH --------------------------------------------------------------------
 hipError_t launch_mh(gm_dtype dt, const TargetDev& tg, const Layout& lay, const MhLaunch& a,
-                     hipStream_t st);
+                     hipStream_t st, LaunchEvents ev = {});
 
 // ---- target evaluation -----------------------------------------------------
 // one leapfrog of n chains, state in HBM (util_device.h leapfrog_hbm_kernel)

@@ -33,6 +33,13 @@ template <class T> struct UserTarget {
     static_assert(LPC == 1 && E == GM_DIM, "user targets run one chain per lane");
     return gm_logp_grad<T>(x, g, params);
   }
+  // one lane per chain: the "part" is the whole log-density
+  template <int LPC> static constexpr bool has_part = true;
+  template <int LPC, int E>
+  __device__ __forceinline__ T eval_part(const T (&x)[E], T (&g)[E], int lane) const {
+    return eval<LPC, E, true>(x, g, lane);
+  }
+  __device__ __forceinline__ T finish(T total) const { return total; }
 };
 }  // namespace gm
 )GMADAPT";

@@ -34,7 +34,6 @@ struct HmcLaunch {
   int collect_from = 0;         // steps s >= collect_from are stored ...
   long long sample_row0 = 0;    // ... at row sample_row0 + (s - collect_from)
   int lf_unroll = 1;            // leapfrog loop unroll (1 or 4; same results)
-  int chains_per_wave = 1;      // 64-lane layouts: 1 (hmc_kernel) or 2 (hmc_kernel_cw); same results
   void* zs = nullptr;           // wide layouts: momentum block scratch [C][S][lanes*elems]
 };
 

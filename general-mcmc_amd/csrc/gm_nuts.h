@@ -18,10 +18,10 @@ struct NutsState {
   void* h_bar = nullptr;    // [C] T   (:582)
   void* mu = nullptr;       // [C] T   (:580)
   void* stk_vec = nullptr;  // [max_depth][3][C][D] T : left-subtree first q, first p, proposal q
-  void* stk_alpha = nullptr;  // [max_depth][C*LPC] T
-  int* stk_n = nullptr;       // [max_depth][C*LPC]
-  int* stk_na = nullptr;      // [max_depth][C*LPC]
-  long long stk_lanes = 0;    // C*LPC the scalar stack was sized for
+  void* stk_alpha = nullptr;  // [max_depth][C] T  (levels held in HBM)
+  int* stk_n = nullptr;       // [max_depth][C]
+  int* stk_na = nullptr;      // [max_depth][C]
+  long long lds_levels_cap = -1;  // subtree-stack levels in LDS: -1 as many as fit
   long long* n_leapfrog = nullptr;  // [C] cumulative leapfrog count
   long long m = 0;            // transitions since the last init_chain_state (:735)
   long long n_discard = 0;    // warm-up length of the current run (:734)

@@ -386,6 +386,30 @@ __device__ __forceinline__ u32x4 draw_block(const PhiloxKeys& K, uint32_t chain,
 }
 #endif
 
+// ---- NUTS per-transition draws (stream spec v3) ----------------------------
+// One Philox block per (chain, transition st), TAG_NUTS_EXP: words x, y are
+// the transition's 64-bit stream key K, words z, w the slice variable's Exp1
+// uniform ((0,1] form). Every other scalar draw of the transition is
+//   h(K, idx) = mix64(K + (idx + 1) * 0x9E3779B97F4A7C15)
+// (SplitMix64's finalizer over a Weyl sequence): doubling j's direction idx
+// 2j, its top-level accept idx 2j + 1, merge m (recursion post-order) idx
+// 64 + m. One Philox per transition instead of one per draw.
+GM_HD uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+GM_HD uint64_t nuts_key(u32x4 w) { return (uint64_t)w.x | ((uint64_t)w.y << 32); }
+template <class T> GM_HD T nuts_u(uint64_t key, uint32_t idx);
+template <> GM_HD double nuts_u<double>(uint64_t key, uint32_t idx) {
+  const uint64_t h = mix64(key + (uint64_t)(idx + 1u) * 0x9E3779B97F4A7C15ull);
+  return (double)(h >> 11) * 1.1102230246251565e-16;
+}
+template <> GM_HD float nuts_u<float>(uint64_t key, uint32_t idx) {
+  const uint64_t h = mix64(key + (uint64_t)(idx + 1u) * 0x9E3779B97F4A7C15ull);
+  return (float)(uint32_t)(h >> 40) * 5.9604644775390625e-08f;
+}
+
 // the S normals of a block
 GM_HD void normals_of(u32x4 x, float (&z)[4]) {
   float c, s;

@@ -152,7 +152,6 @@ struct gm_sampler {
   size_t zs_bytes = 0;
   Layout lay;
   long long steps_per_launch = 1000;
-  int chains_per_wave = 0;  // HMC 64-lane layouts: 0 automatic, 1 or 2
   std::vector<hipEvent_t> evs;
   double last_ms = 0;
   long long last_launches = 0;
@@ -562,13 +561,6 @@ int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems) {
   return GM_OK;
 }
 
-int gm_sampler_set_chains_per_wave(gm_sampler* s, int32_t chains_per_wave) {
-  GM_REQ(s, "sampler is NULL");
-  GM_REQ(chains_per_wave >= 0 && chains_per_wave <= 2, "chains_per_wave must be 0 (automatic), 1 or 2");
-  s->chains_per_wave = chains_per_wave;
-  return GM_OK;
-}
-
 int gm_sampler_set_steps_per_launch(gm_sampler* s, int64_t steps) {
   GM_REQ(s, "sampler is NULL");
   // the kernels take a launch's transition count as an int
@@ -606,13 +598,6 @@ static int hmc_lf_unroll(long long waves) {
   return waves <= simds ? 4 : 1;
 }
 
-// Chains per wave of the 64-lane HMC kernel (automatic choice; identical
-// results either way): see hmc_kernel_cw.
-static int hmc_chains_per_wave(const gm_sampler* s) {
-  (void)s;
-  return 1;
-}
-
 // hipSetDevice only when the calling thread is on another device (the call
 // is on every run's path)
 static hipError_t use_device(int dev) {
@@ -621,6 +606,22 @@ static hipError_t use_device(int dev) {
   const hipError_t e = hipSetDevice(dev);
   if (e == hipSuccess) cur = dev;
   return e;
+}
+
+// The end of a run: poll the stop event (the run's last launch completing)
+// instead of a blocking stream wait, whose wake-up after an idle stretch
+// costs microseconds on every run; then drain the stream.
+static hipError_t wait_event(hipEvent_t ev, hipStream_t st) {
+#ifdef GM_AB_BLOCKSYNC  // A/B builds only
+  (void)ev;
+  return hipStreamSynchronize(st);
+#else
+  hipError_t e;
+  while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
+  }
+  if (e != hipSuccess) return e;
+  return hipStreamSynchronize(st);
+#endif
 }
 
 // One event pair per run (before the first launch, after the last): the
@@ -657,8 +658,10 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
   int rc = ensure_run_events(s);
   if (rc) return rc;
   const int lf_unroll = s->kind == K_HMC ? hmc_lf_unroll((s->C * s->lay.lanes + 63) / 64) : 1;
-  GM_HIP(hipEventRecord(s->evs[0], s->stream));
   for (long long start = 0; start < total; start += chunk) {
+    LaunchEvents ev;  // start with the first launch, stop with the last
+    if (start == 0) ev.start = s->evs[0];
+    if (start + chunk >= total) ev.stop = s->evs[1];
     const long long n = total - start < chunk ? total - start : chunk;
     long long cf = collect_from - start;
     if (cf < 0) cf = 0;
@@ -683,17 +686,13 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
       a.collect_from = (int)cf;
       a.sample_row0 = row0;
       a.lf_unroll = lf_unroll;
-      a.chains_per_wave = s->chains_per_wave ? s->chains_per_wave : hmc_chains_per_wave(s);
-#ifdef GM_AB_CW
-      a.chains_per_wave = GM_AB_CW;  // A/B builds only
-#endif
       if (layout_is_wide(s->lay)) {
         const size_t need = (size_t)s->C * (s->dt == GM_F32 ? 4 : 2) * s->lay.lanes * s->lay.elems * s->esz;
         rc = ensure_buf(&s->d_zs, &s->zs_bytes, need);
         if (rc) return rc;
         a.zs = s->d_zs;
       }
-      e = launch_hmc(s->dt, s->tg, s->lay, a, s->stream);
+      e = launch_hmc(s->dt, s->tg, s->lay, a, s->stream, ev);
     } else {
       MhLaunch a;
       a.q = s->d_q;
@@ -713,7 +712,7 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
         a.trk = *trk;
         a.trk.n0 = trk->n0 + (unsigned long long)start;
       }
-      e = launch_mh(s->dt, s->tg, s->lay, a, s->stream);
+      e = launch_mh(s->dt, s->tg, s->lay, a, s->stream, ev);
     }
     if (e != hipSuccess) {
       set_error(std::string("kernel launch failed: ") + hipGetErrorString(e));
@@ -724,10 +723,9 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
       if (rc) return rc;
     }
   }
-  GM_HIP(hipEventRecord(s->evs[1], s->stream));
   s->step += total;
   s->total_steps += total;
-  GM_HIP(hipStreamSynchronize(s->stream));
+  GM_HIP(wait_event(s->evs[1], s->stream));
   float t = 0;
   GM_HIP(hipEventElapsedTime(&t, s->evs[0], s->evs[1]));
   s->last_ms = t;
@@ -1080,6 +1078,14 @@ int gm_nuts_set_mass_adaptation(gm_sampler* s, int32_t mode, int64_t start_buffe
   if (mode == 2 && s->D > dense_max_dim) mode = 1;
   return nuts_set_mass(&s->nuts, s->dt, s->C, s->D, mode, start_buffer, end_buffer, initial_window,
                        regularize, jitter);
+}
+
+int gm_nuts_set_lds_levels(gm_sampler* s, int32_t levels) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");
+  GM_REQ(levels >= -1 && levels <= NUTS_MAX_DEPTH_LIMIT, "levels must be -1 (automatic) or 0..30");
+  s->nuts.lds_levels_cap = levels;
+  return GM_OK;
 }
 
 int gm_nuts_get_mass(gm_sampler* s, int32_t* mode, int32_t* kind, void* dinv, void* dsqrt, void* minv,

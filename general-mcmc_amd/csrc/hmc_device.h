@@ -224,270 +224,6 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
 }
 
 // ---------------------------------------------------------------------------
-// hmc_kernel_cw: the 64-lane layouts (LPC = 64) with CW chains per wave.
-// Lane l holds coordinates [l*E, (l+1)*E) of each of the wave's CW chains,
-// and every step of the transition is issued for the CW chains back to back:
-// CW independent dependency chains per wave. The leapfrog of one chain is a
-// chain of ~11 dependent VALU operations (two of them DPP-fed); with one chain
-// per wave only the other waves of the SIMD can fill a dependent operation's
-// latency, and the 64-D / 4096-chain workload has just 4 waves per SIMD. With
-// CW = 2 it has 2 waves per SIMD, each issuing two independent streams.
-// Per-chain arithmetic and summation order are those of hmc_kernel (bit-
-// identical samples); the per-chain sums of the CW chains are reduced
-// interleaved (group_sum_n). The accept branch stays wave-uniform per chain.
-template <class T, int E, int CW, class TG>
-__global__ __launch_bounds__(256) void hmc_kernel_cw(HmcLaunch a, TG tg_) {
-  constexpr int LPC = 64;
-  const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long wv = gtid >> 6;
-  const int lane = (int)(gtid & 63);
-  const auto tg = tg_.template bind<LPC, E>(lane);
-  const long long cbase = wv * CW;
-  if (cbase >= a.C) return;  // whole waves leave together
-  const int D = a.D;
-  T* __restrict__ qs = (T*)a.q;
-  const T eps = (T)a.eps;
-  const T half = (T)0.5 * eps;  // batched_hmc.rs:167
-  long long cc[CW];             // chain of slot k (a missing last chain repeats the previous one, never stored)
-  bool live[CW];
-  uint32_t cid[CW], ucid[CW];
-#pragma unroll
-  for (int k = 0; k < CW; ++k) {
-    live[k] = cbase + k < a.C;
-    cc[k] = live[k] ? cbase + k : a.C - 1;
-    cid[k] = a.chain_offset + (uint32_t)cc[k];
-    ucid[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)cid[k]);
-  }
-  T q[CW][E], g[CW][E], p1[CW][E], q1[CW][E], g1[CW][E];
-#pragma unroll
-  for (int k = 0; k < CW; ++k)
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int i = lane * E + e;
-      q[k][e] = (i < D) ? qs[cc[k] * D + i] : (T)0;
-    }
-  T lp[CW];
-  {
-    T parts[CW];
-#pragma unroll
-    for (int k = 0; k < CW; ++k) parts[k] = tg.template eval_part<LPC, E>(q[k], g[k], lane);
-    group_sum_n<LPC>(parts);
-#pragma unroll
-    for (int k = 0; k < CW; ++k) lp[k] = tg.finish(parts[k]);
-  }
-  long long acc[CW];
-#pragma unroll
-  for (int k = 0; k < CW; ++k) acc[k] = 0;
-  constexpr int S = Blk<T>::S;
-  const PhiloxKeys pk = philox_keys(a.seed);
-  T zsA[CW][E][S], kesA[CW][S], lusA[CW][S];
-  T zsB[CW][E][S], kesB[CW][S], lusB[CW][S];
-  bool hasB = false;
-  const int phase = (int)(wv % S);  // staggered prefetch (see hmc_kernel)
-  auto fill = [&](T (&zs)[CW][E][S], T (&kes)[CW][S], T (&lus)[CW][S], uint64_t blk) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < CW; ++k)
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int i = lane * E + e;
-        normals_of(draw_block(pk, cid[k], blk, TAG_MOM, (uint32_t)i), zs[k][e]);
-#pragma unroll
-        for (int j = 0; j < S; ++j) zs[k][e][j] = (i < D) ? zs[k][e][j] : (T)0;
-      }
-    T kp[CW * S];
-#pragma unroll
-    for (int k = 0; k < CW; ++k)
-#pragma unroll
-      for (int j = 0; j < S; ++j)
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const T sq = zs[k][e][j] * zs[k][e][j];
-          kp[k * S + j] = (e == 0) ? sq : kp[k * S + j] + sq;
-        }
-    group_sum_n<LPC>(kp);
-#pragma unroll
-    for (int k = 0; k < CW; ++k)
-#pragma unroll
-      for (int j = 0; j < S; ++j) kes[k][j] = kp[k * S + j] * (T)0.5;
-    // the CW*S accept log-uniforms: lane k*S+j evaluates ln u_{k,j} in one
-    // VALU pass, each read back as a scalar
-    T um = (T)0;
-#pragma unroll
-    for (int k = 0; k < CW; ++k) {
-      T us[S];
-      uniforms_of(draw_block(a.seed, ucid[k], blk, TAG_ACC, 0u), us);
-#pragma unroll
-      for (int j = 0; j < S; ++j) um = (lane == k * S + j) ? us[j] : um;
-    }
-    const T lm = glog_unif(um);
-#pragma unroll
-    for (int k = 0; k < CW; ++k)
-#pragma unroll
-      for (int j = 0; j < S; ++j) lus[k][j] = lane_k(lm, k * S + j);
-  };
-  const uint64_t st_end = a.step0 + (uint64_t)a.n_steps;
-
-  for (int s = 0; s < a.n_steps; ++s) {
-    const uint64_t st = a.step0 + (uint64_t)s;
-    const int k0 = (int)(st % S);
-    if (s == 0 || k0 == 0) {
-      if (s > 0 && hasB) {
-#pragma unroll
-        for (int k = 0; k < CW; ++k)
-#pragma unroll
-          for (int j = 0; j < S; ++j) {
-#pragma unroll
-            for (int e = 0; e < E; ++e) zsA[k][e][j] = zsB[k][e][j];
-            kesA[k][j] = kesB[k][j];
-            lusA[k][j] = lusB[k][j];
-          }
-      } else {
-        fill(zsA, kesA, lusA, st / S);
-#pragma unroll
-        for (int k = 0; k < CW; ++k) {
-#pragma unroll
-          for (int e = 0; e < E; ++e) skip_front(zsA[k][e], k0);
-          skip_front(kesA[k], k0);
-          skip_front(lusA[k], k0);
-        }
-      }
-      hasB = false;
-    }
-    T ke0[CW], lnu[CW];
-#pragma unroll
-    for (int k = 0; k < CW; ++k) {
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        p1[k][e] = zsA[k][e][0];
-        shift_front(zsA[k][e]);
-      }
-      ke0[k] = kesA[k][0];
-      lnu[k] = lusA[k][0];
-      shift_front(kesA[k]);
-      shift_front(lusA[k]);
-    }
-    if (!hasB && k0 == phase && st - (uint64_t)k0 + S < st_end) {
-      fill(zsB, kesB, lusB, st / S + 1);
-      hasB = true;
-    }
-    T gh[CW][E];
-#pragma unroll
-    for (int k = 0; k < CW; ++k)
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-        q1[k][e] = q[k][e];
-        g1[k][e] = g[k][e];
-        gh[k][e] = g1[k][e] * half;
-      }
-    for (int l = 0; l + 1 < a.L; ++l) {
-#pragma unroll
-      for (int k = 0; k < CW; ++k)
-#pragma unroll
-        for (int e = 0; e < E; ++e) p1[k][e] = p1[k][e] + gh[k][e];
-#pragma unroll
-      for (int k = 0; k < CW; ++k)
-#pragma unroll
-        for (int e = 0; e < E; ++e) q1[k][e] = q1[k][e] + p1[k][e] * eps;
-#pragma unroll
-      for (int k = 0; k < CW; ++k) tg.template eval<LPC, E, false>(q1[k], g1[k], lane);
-#pragma unroll
-      for (int k = 0; k < CW; ++k)
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          gh[k][e] = g1[k][e] * half;
-          p1[k][e] = p1[k][e] + gh[k][e];
-        }
-    }
-    T lp1[CW], ke1[CW];
-    if (a.L >= 1) {
-      T sums[2 * CW];
-#pragma unroll
-      for (int k = 0; k < CW; ++k) {
-#pragma unroll
-        for (int e = 0; e < E; ++e) p1[k][e] = p1[k][e] + gh[k][e];
-#pragma unroll
-        for (int e = 0; e < E; ++e) q1[k][e] = q1[k][e] + p1[k][e] * eps;
-      }
-#pragma unroll
-      for (int k = 0; k < CW; ++k) sums[2 * k] = tg.template eval_part<LPC, E>(q1[k], g1[k], lane);
-#pragma unroll
-      for (int k = 0; k < CW; ++k) {
-        T kq = (T)0;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          p1[k][e] = p1[k][e] + g1[k][e] * half;
-          const T sq = p1[k][e] * p1[k][e];
-          kq = (e == 0) ? sq : kq + sq;
-        }
-        sums[2 * k + 1] = kq;
-      }
-      group_sum_n<LPC>(sums);
-#pragma unroll
-      for (int k = 0; k < CW; ++k) {
-        lp1[k] = tg.finish(sums[2 * k]);
-        ke1[k] = sums[2 * k + 1] * (T)0.5;
-      }
-    } else {
-      T kq[CW];
-#pragma unroll
-      for (int k = 0; k < CW; ++k) {
-        kq[k] = (T)0;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const T sq = p1[k][e] * p1[k][e];
-          kq[k] = (e == 0) ? sq : kq[k] + sq;
-        }
-      }
-      group_sum_n<LPC>(kq);
-#pragma unroll
-      for (int k = 0; k < CW; ++k) {
-        lp1[k] = lp[k];
-        ke1[k] = kq[k] * (T)0.5;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < CW; ++k) {
-      const T log_alpha = (lp1[k] - lp[k]) + (ke0[k] - ke1[k]);
-      if (log_alpha >= lnu[k]) {  // wave-uniform per chain
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          q[k][e] = q1[k][e];
-          g[k][e] = g1[k][e];
-        }
-        lp[k] = lp1[k];
-        ++acc[k];
-      }
-    }
-    if (s >= a.collect_from) {
-      const long long row = a.sample_row0 + (s - a.collect_from);
-#pragma unroll
-      for (int k = 0; k < CW; ++k) {
-        if (!live[k]) continue;
-        T* __restrict__ out = (T*)a.samples + (row * a.C + cc[k]) * D;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const int i = lane * E + e;
-          if (i < D) out[i] = q[k][e];
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < CW; ++k) {
-    if (!live[k]) continue;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int i = lane * E + e;
-      if (i < D) qs[cc[k] * D + i] = q[k][e];
-    }
-    if (lane == 0) {
-      ((T*)a.logp)[cc[k]] = lp[k];
-      a.accepts[cc[k]] += acc[k];
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // hmc_wide_kernel: the same transition for dim > 1024, one chain per
 // workgroup of W = blockDim/64 waves (WideCtx in gm_device.h). The per-step
 // momenta of a draw block (S transitions) go to a per-chain scratch in HBM

@@ -22,36 +22,25 @@
 
 namespace gm {
 hipError_t launch_hmc(gm_dtype dt, const TargetDev& tg, const Layout& lay, const HmcLaunch& a,
-                      hipStream_t st) {
+                      hipStream_t st, LaunchEvents ev) {
   if (tg.kind == GM_TARGET_CUSTOM) {  // user target, runtime-compiled (gm_jit.cpp)
     HmcLaunch aa = a;
     UserTargetArg ut{tg.params, tg.D};
     void* args[] = {&aa, &ut};
-    return jit_launch(JIT_HMC, dt, tg, (unsigned)((a.C + 255) / 256), 256, 0, st, args);
+    return with_events(ev, st, [&] {
+      return jit_launch(JIT_HMC, dt, tg, (unsigned)((a.C + 255) / 256), 256, 0, st, args);
+    });
   }
   if (layout_is_wide(lay)) {
     return dispatch_wide(dt, tg, lay, [&]<class T, int E, class TG>(TG t) -> hipError_t {
-      hipLaunchKernelGGL((hmc_wide_kernel<T, E, TG>), dim3((unsigned)a.C), dim3(lay.lanes), 0, st, a, t);
-      return hipGetLastError();
+      return launch_timed(hmc_wide_kernel<T, E, TG>, dim3((unsigned)a.C), dim3(lay.lanes), 0, st, ev, a, t);
     });
   }
   return dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
     const size_t lds = t.template lds_bytes<LPC, E>();
-    if constexpr (LPC == 64) {
-      using TL = decltype(t.template bind<LPC, E>(0));
-      if constexpr (requires { TL::template has_part<LPC>; }) {
-        if (a.chains_per_wave == 2) {  // two chains per wave (hmc_kernel_cw)
-          const long long threads = (a.C + 1) / 2 * 64;
-          const unsigned blocks = (unsigned)((threads + 255) / 256);
-          hipLaunchKernelGGL((hmc_kernel_cw<T, E, 2, TG>), dim3(blocks), dim3(256), lds, st, a, t);
-          return hipGetLastError();
-        }
-      }
-    }
     const long long threads = a.C * LPC;
     const unsigned blocks = (unsigned)((threads + 255) / 256);
-    hipLaunchKernelGGL((hmc_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), lds, st, a, t);
-    return hipGetLastError();
+    return launch_timed(hmc_kernel<T, LPC, E, TG>, dim3(blocks), dim3(256), lds, st, ev, a, t);
   });
 }
 

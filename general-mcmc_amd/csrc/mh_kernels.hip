@@ -17,19 +17,20 @@
 
 namespace gm {
 hipError_t launch_mh(gm_dtype dt, const TargetDev& tg, const Layout& lay, const MhLaunch& a,
-                     hipStream_t st) {
+                     hipStream_t st, LaunchEvents ev) {
   if (tg.kind == GM_TARGET_CUSTOM) {  // user target, runtime-compiled (gm_jit.cpp)
     MhLaunch aa = a;
     UserTargetArg ut{tg.params, tg.D};
     void* args[] = {&aa, &ut};
-    return jit_launch(JIT_MH, dt, tg, (unsigned)((a.C + 255) / 256), 256, 0, st, args);
+    return with_events(ev, st, [&] {
+      return jit_launch(JIT_MH, dt, tg, (unsigned)((a.C + 255) / 256), 256, 0, st, args);
+    });
   }
   return dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
     const long long threads = a.C * LPC;
     const unsigned blocks = (unsigned)((threads + 255) / 256);
     const size_t lds = t.template lds_bytes<LPC, E>();
-    hipLaunchKernelGGL((mh_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), lds, st, a, t);
-    return hipGetLastError();
+    return launch_timed(mh_kernel<T, LPC, E, TG>, dim3(blocks), dim3(256), lds, st, ev, a, t);
   });
 }
 

@@ -168,39 +168,27 @@ __device__ __forceinline__ T leapfrog_m(const TG& tg, const MassDev<T, E>& M, T 
   return lp;
 }
 
-// leapfrog_m followed by kinetic_m at the new point. With the identity
-// metric and a target that exposes its unreduced log-density term
-// (eval_part / finish), both per-chain sums are reduced together: the same
-// stages and bits as the two separate reductions.
-template <int LPC, int E, class T, class TG>
-__device__ __forceinline__ void leaf_leapfrog(const TG& tg, const MassDev<T, E>& M, T (&q)[E], T (&p)[E],
-                                              T (&g)[E], T epsv, int lane, T& lp, T& kin) {
-  using TL = typename Bare<TG>::type;
-  if constexpr (requires { TL::template has_part<LPC>; }) {
-    if constexpr (TL::template has_part<LPC>) {
-      if (M.kind == 0) {
-        const T h = epsv * (T)0.5;
+// Unreduced per-lane term of MassMatrix::kinetic (:226-253) without the
+// 0.5: sum_e p_e^2 (identity), p_e^2 inv_e (diagonal), p_e (M^-1 p)_e
+// (dense); kinetic = 0.5 * group_sum(part), the operations of kinetic_m.
+template <int LPC, int E, class T>
+__device__ __forceinline__ T kin_part_m(const MassDev<T, E>& M, const T (&p)[E], int lane) {
+  T t[E];
+  if (M.kind == 0) {
 #pragma unroll
-        for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
+    for (int e = 0; e < E; ++e) t[e] = p[e] * p[e];
+  } else if (M.kind == 1) {
 #pragma unroll
-        for (int e = 0; e < E; ++e) q[e] = q[e] + p[e] * epsv;
-        T sums[2];
-        sums[0] = tg.template eval_part<LPC, E>(q, g, lane);
+    for (int e = 0; e < E; ++e) t[e] = p[e] * p[e] * M.inv[e];
+  } else {
+    inv_mul<LPC, E>(M, p, t, lane);
 #pragma unroll
-        for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
-        T kp = p[0] * p[0];
-#pragma unroll
-        for (int e = 1; e < E; ++e) kp = kp + p[e] * p[e];
-        sums[1] = kp;
-        group_sum_n<LPC>(sums);
-        lp = tg.finish(sums[0]);
-        kin = (T)0.5 * sums[1];
-        return;
-      }
-    }
+    for (int e = 0; e < E; ++e) t[e] = p[e] * t[e];
   }
-  lp = leapfrog_m<LPC, E>(tg, M, q, p, g, epsv, lane);
-  kin = kinetic_m<LPC, E>(M, p, lane);
+  T part = t[0];
+#pragma unroll
+  for (int e = 1; e < E; ++e) part = part + t[e];
+  return part;
 }
 
 // stop_criterion_with_mass (:1354-1378), the top-level U-turn
@@ -278,6 +266,27 @@ __device__ T find_reasonable_epsilon(const TG& tg, const T (&q0)[E], const T (&p
   return eps;
 }
 
+
+// ---------------------------------------------------------------------------
+// nuts_kernel: every chain's NUTS transitions, lockstep by leaf.
+//
+// Each iteration of the main loop performs ONE target evaluation for every
+// chain of the wave: the next leaf's leapfrog for a chain inside its tree, or
+// the evaluation at q that starts a transition (generic_nuts.rs:758-768) for
+// a chain that finished its previous one. Chains therefore do not wait for
+// the deepest tree of their wave at every transition: a wave runs until its
+// chains have each done n_steps transitions, and only the per-leaf merge
+// climb, the end of a doubling and the end of a transition diverge.
+//
+// The tree (build_tree_with_mass, generic_nuts.rs:1153-1341) is evaluated
+// iteratively: leaves in trajectory order; a leaf then climbs the levels of
+// its doubling, merging with the stored left sibling of every level where it
+// completes a right child (the recursion's post-order, so the merge draws are
+// the recursion's) and storing itself where it is a left child. A truncated
+// subtree (s' = false) climbs without storing (its parent builds no right
+// half) and ends the doubling. The trajectory ends live in registers as the
+// edge (the end being integrated, side v) and the far end; a direction change
+// swaps them.
 template <class T, int LPC, int E, class TG>
 __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -291,18 +300,20 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   T* __restrict__ qs = (T*)a.q;
   T* __restrict__ svec = (T*)a.stk_vec;
   T* __restrict__ salpha = (T*)a.stk_alpha;
-  const long long slane = c * LPC + lane;  // scalar-stack slot of this lane
-  const long long CL = C * LPC;
-  // Subtree stack. Level k < KL: LDS, [k][field][thread*E + e] vectors and
-  // [k][thread] scalars of this block (a lane reads back only what it wrote:
-  // no synchronisation). Deeper levels: HBM [k][field][chain][coord].
+  // Subtree stack. Level k < KL: LDS, vectors [k][field][thread*E + e] of
+  // this block, scalars [k][chain in block] (every lane of a chain writes the
+  // same value); a lane reads back only what it or its group wrote, so no
+  // synchronisation. Deeper levels: HBM, vectors [k][field][chain][coord],
+  // scalars [k][chain].
   constexpr int NT = 256;  // threads per block (launch_nuts)
+  constexpr int CPB = NT / LPC;
   const int KL = a.lds_levels;
   T* __restrict__ lvec = (T*)(gm_dyn_lds + a.lds_stack_off);
   T* __restrict__ lalpha = lvec + (long long)KL * 3 * NT * E;
-  int* __restrict__ lnn = (int*)(lalpha + KL * NT);
-  int* __restrict__ lnna = lnn + KL * NT;
+  int* __restrict__ lnn = (int*)(lalpha + KL * CPB);
+  int* __restrict__ lnna = lnn + KL * CPB;
   const int tix = threadIdx.x;
+  const int cib = tix / LPC;  // chain in block
   auto stack_store = [&](int k, const T (&f0)[E], const T (&f1)[E], const T (&f2)[E], T al, int nn,
                          int nna) __attribute__((always_inline)) {
     if (k < KL) {
@@ -313,9 +324,9 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
         v[NT * E + e] = f1[e];
         v[2 * NT * E + e] = f2[e];
       }
-      lalpha[k * NT + tix] = al;
-      lnn[k * NT + tix] = nn;
-      lnna[k * NT + tix] = nna;
+      lalpha[k * CPB + cib] = al;
+      lnn[k * CPB + cib] = nn;
+      lnna[k * CPB + cib] = nna;
     } else {
       T* sv = svec + ((long long)(k * 3) * C + c) * D;
 #pragma unroll
@@ -327,9 +338,9 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
           sv[2 * C * D + i] = f2[e];
         }
       }
-      salpha[k * CL + slane] = al;
-      a.stk_n[k * CL + slane] = nn;
-      a.stk_na[k * CL + slane] = nna;
+      salpha[k * C + c] = al;
+      a.stk_n[k * C + c] = nn;
+      a.stk_na[k * C + c] = nna;
     }
   };
   // field f (0 first q, 1 first p, 2 proposal) of level k
@@ -349,13 +360,13 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   };
   auto stack_scalars = [&](int k, T& al, long long& nn, long long& nna) __attribute__((always_inline)) {
     if (k < KL) {
-      al = lalpha[k * NT + tix];
-      nn = lnn[k * NT + tix];
-      nna = lnna[k * NT + tix];
+      al = lalpha[k * CPB + cib];
+      nn = lnn[k * CPB + cib];
+      nna = lnna[k * CPB + cib];
     } else {
-      al = salpha[k * CL + slane];
-      nn = a.stk_n[k * CL + slane];
-      nna = a.stk_na[k * CL + slane];
+      al = salpha[k * C + c];
+      nn = a.stk_n[k * C + c];
+      nna = a.stk_na[k * C + c];
     }
   };
 
@@ -434,12 +445,36 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   const bool track = a.trk.mean != nullptr;  // run_progress (generic_nuts.rs:688-704)
   ChainTrack<LPC, E> tr;
   if (track) tr.load(a.trk, c, lane, D);
-  for (int s = 0; s < a.n_steps; ++s) {
+
+  // per-chain loop state
+  int s = 0;             // transitions completed in this launch
+  bool starting = true;  // the next evaluation starts transition s
+  T p0[E];               // the transition's momentum (starting chains)
+  T qe[E], pe[E], ge[E];  // edge: the trajectory end on side v (being integrated)
+  T qf[E], pf[E], gf[E];  // the far end
+  int v = 1, j = 0;
+  long long l = 0, n = 1;
+  T joint0 = (T)0, logu = (T)0;
+  uint64_t key = 0;
+  uint32_t merge_ctr = 0;
+  T fq[E], fp[E], pr[E];  // current subtree: first q, first p, proposal
+  long long tn = 0, tna = 0;
+  bool ts = true;
+  T ta = (T)0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    qe[e] = pe[e] = ge[e] = qf[e] = pf[e] = gf[e] = fq[e] = fp[e] = pr[e] = p0[e] = (T)0;
+  }
+
+  while (true) {
+    const bool live = s < a.n_steps;
+    if (__builtin_amdgcn_ballot_w64(live) == 0) break;  // every chain of the wave is done
     const uint64_t st = a.step0 + (uint64_t)s;
-    const long long m = a.m0 + s + 1;
-    // --- momentum, slice (generic_nuts.rs:758-768)
-    T p0[E], g0[E];
-    {
+    const T epsv = (T)v * eps;
+    const T h = epsv * (T)0.5;
+    // --- the evaluation point: q (a starting transition) or the next leaf
+    T x[E], gx[E];
+    if (live && starting) {  // momentum (generic_nuts.rs:758-762)
       T z[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -448,105 +483,145 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       }
       momentum_from<LPC, E>(M, z, p0, lane);
     }
-    const T logp0 = tg.template eval<LPC, E, true>(q, g0, lane);
-    const T joint0 = logp0 - kinetic_m<LPC, E>(M, p0, lane);
-    const T logu = joint0 - exp1<T>(a.seed, cid, st, TAG_NUTS_EXP, 0u);
-    // trajectory ends
-    T qm[E], pm[E], gm_[E], qp[E], pp[E], gp[E];
+    if (live && !starting) {  // leapfrog_with_mass (:1396-1418): kick, drift by M^-1 p
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      qm[e] = q[e]; qp[e] = q[e];
-      pm[e] = p0[e]; pp[e] = p0[e];
-      gm_[e] = g0[e]; gp[e] = g0[e];
+      for (int e = 0; e < E; ++e) pe[e] = pe[e] + ge[e] * h;
+      T vv[E];
+      inv_mul<LPC, E>(M, pe, vv, lane);
+#pragma unroll
+      for (int e = 0; e < E; ++e) qe[e] = qe[e] + vv[e] * epsv;
     }
-    long long n = 1;
-    bool s_ok = true;
-    T alpha = (T)0;
-    long long n_alpha = 0;
-    uint32_t merge_ctr = 0;
-    int j = 0;
-    while (s_ok && j < a.max_depth) {
-      const T u1 = uniform_co<T>(a.seed, cid, st, TAG_NUTS_DIR, (uint32_t)j);
-      const int v = (u1 < (T)0.5) ? 1 : -1;
-      const T epsv = (T)v * eps;
-      // edge state = the trajectory end on side v
-      T qe[E], pe[E], ge[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[e] = starting ? q[e] : qe[e];
+    T sums[2];
+    sums[0] = tg.template eval_part<LPC, E>(x, gx, lane);
+    if (live && !starting) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) pe[e] = pe[e] + gx[e] * h;
+    }
+    {
+      T pk[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) pk[e] = starting ? p0[e] : pe[e];
+      sums[1] = kin_part_m<LPC, E>(M, pk, lane);
+    }
+    group_sum_n<LPC>(sums);  // log-density and kinetic energy, reduced together
+    const T lp = tg.finish(sums[0]);
+    const T kin = (T)0.5 * sums[1];
+    if (!live) continue;
+
+    if (starting) {
+      // --- transition start: slice variable, trajectory ends (:764-781)
+      joint0 = lp - kin;
+      const u32x4 kw = draw_block(a.seed, cid, st, TAG_NUTS_EXP, 0u);
+      key = nuts_key(kw);
+      logu = joint0 + glog_pos(Unif<T>::oc(kw.z, kw.w));  // joint - Exp1
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        qe[e] = v > 0 ? qp[e] : qm[e];
-        pe[e] = v > 0 ? pp[e] : pm[e];
-        ge[e] = v > 0 ? gp[e] : gm_[e];
+        qe[e] = q[e]; pe[e] = p0[e]; ge[e] = gx[e];
+        qf[e] = q[e]; pf[e] = p0[e]; gf[e] = gx[e];
       }
-      // current subtree T
-      T fq[E], fp[E], pr[E];
-      long long tn = 0;
-      bool ts = true;
-      T ta = (T)0;
-      long long tna = 0;
-      const long long nleaves = 1LL << j;
-      for (long long l = 0; l < nleaves; ++l) {
-        T lp, kin;
-        leaf_leapfrog<LPC, E>(tg, M, qe, pe, ge, epsv, lane, lp, kin);
-        ++nlf;
-        const T joint = lp - kin;
-        tn = (logu < joint) ? 1 : 0;
-        ts = (logu - (T)1000) < joint;
-        ta = rust_min1(gexp(joint - joint0));
-        tna = 1;
+      n = 1;
+      j = 0;
+      l = 0;
+      merge_ctr = 0;
+      v = (nuts_u<T>(key, 0u) < (T)0.5) ? 1 : -1;  // direction of doubling 0 (:783-784)
+      starting = false;
+      continue;
+    }
+
+    // --- a leaf (build_tree_with_mass base case, :1187-1212)
+    ++nlf;
 #pragma unroll
-        for (int e = 0; e < E; ++e) { fq[e] = qe[e]; fp[e] = pe[e]; pr[e] = qe[e]; }
-        bool done = false;
-        int k = 0;
-        while (true) {
-          if (k == j) { done = true; break; }
-          if (((l >> k) & 1) == 0) {  // left child at level k
-            // A truncated left subtree: its parent builds no right half and
-            // returns it unchanged; going up, it is merged wherever that
-            // parent is itself a right child (the recursion's post-order).
-            if (!ts) { ++k; continue; }
-            stack_store(k, fq, fp, pr, ta, (int)tn, (int)tna);
-            break;
-          }
-          // right child: merge with the stored left sibling (generic_nuts.rs:1251-1323)
-          T lq[E], lpv[E];
-          stack_vec(k, 0, lq);
-          stack_vec(k, 1, lpv);
-          long long ln_, lna;
-          T lal;
-          stack_scalars(k, lal, ln_, lna);
-          const double u = uniform_co<double>(a.seed, cid, st, TAG_NUTS_MRG, merge_ctr++);
-          const long long den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
-          if (!(u < (double)tn / (double)den)) stack_vec(k, 2, pr);
-          tn = ln_ + tn;
-          if (ts) ts = (v > 0) ? no_uturn<LPC, E>(lq, qe, lpv, pe) : no_uturn<LPC, E>(qe, lq, pe, lpv);
-          ta = lal + ta;
-          tna = lna + tna;
+    for (int e = 0; e < E; ++e) ge[e] = gx[e];
+    const T joint = lp - kin;
+    tn = (logu < joint) ? 1 : 0;
+    ts = (logu - (T)1000) < joint;
+    ta = rust_min1(gexp(joint - joint0));
+    tna = 1;
 #pragma unroll
-          for (int e = 0; e < E; ++e) { fq[e] = lq[e]; fp[e] = lpv[e]; }
-          ++k;
-        }
-        if (done) break;
+    for (int e = 0; e < E; ++e) { fq[e] = qe[e]; fp[e] = pe[e]; pr[e] = qe[e]; }
+    // climb: merge with the stored left siblings this leaf completes
+    bool done = false;
+    int k = 0;
+    while (true) {
+      if (k == j) { done = true; break; }
+      if (((l >> k) & 1) == 0) {  // left child at level k
+        // A truncated left subtree: its parent builds no right half and
+        // returns it unchanged; going up, it is merged wherever that parent
+        // is itself a right child (the recursion's post-order).
+        if (!ts) { ++k; continue; }
+        stack_store(k, fq, fp, pr, ta, (int)tn, (int)tna);
+        break;
       }
-      // the new trajectory end on side v is the last leaf integrated
+      // right child: merge with the stored left sibling (:1251-1323)
+      T lq[E], lpv[E];
+      stack_vec(k, 0, lq);
+      stack_vec(k, 1, lpv);
+      long long ln_, lna;
+      T lal;
+      stack_scalars(k, lal, ln_, lna);
+      const double u = nuts_u<double>(key, 64u + merge_ctr++);
+      const long long den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
+      if (!(u < (double)tn / (double)den)) stack_vec(k, 2, pr);
+      tn = ln_ + tn;
+      if (ts) ts = (v > 0) ? no_uturn<LPC, E>(lq, qe, lpv, pe) : no_uturn<LPC, E>(qe, lq, pe, lpv);
+      ta = lal + ta;
+      tna = lna + tna;
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        if (v > 0) { qp[e] = qe[e]; pp[e] = pe[e]; gp[e] = ge[e]; }
-        else { qm[e] = qe[e]; pm[e] = pe[e]; gm_[e] = ge[e]; }
-      }
-      alpha = ta;
-      n_alpha = tna;
+      for (int e = 0; e < E; ++e) { fq[e] = lq[e]; fp[e] = lpv[e]; }
+      ++k;
+    }
+    if (!done) {
+      ++l;
+      continue;
+    }
+
+    // --- the doubling is complete (or truncated): top level (:785-880).
+    // The new end on side v is the edge; alpha / n_alpha are this subtree's.
+    const T alpha = ta;
+    const long long n_alpha = tna;
+    {
       const T tmp = rust_min1((T)tn / (T)n);
-      const T u2 = uniform_co<T>(a.seed, cid, st, TAG_NUTS_TOP, (uint32_t)j);
+      const T u2 = nuts_u<T>(key, 2u * (uint32_t)j + 1u);
       if (ts && (u2 < tmp)) {
 #pragma unroll
         for (int e = 0; e < E; ++e) q[e] = pr[e];
         ++acc;
       }
       n += tn;
-      s_ok = ts && no_uturn_m<LPC, E>(M, qm, qp, pm, pp, lane);
+      bool s_ok = ts;
+      if (s_ok) {
+        T qmv[E], qpv[E], pmv[E], ppv[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          qmv[e] = v > 0 ? qf[e] : qe[e];
+          qpv[e] = v > 0 ? qe[e] : qf[e];
+          pmv[e] = v > 0 ? pf[e] : pe[e];
+          ppv[e] = v > 0 ? pe[e] : pf[e];
+        }
+        s_ok = no_uturn_m<LPC, E>(M, qmv, qpv, pmv, ppv, lane);
+      }
       ++j;
+      if (s_ok && j < a.max_depth) {  // next doubling
+        const int v2 = (nuts_u<T>(key, 2u * (uint32_t)j) < (T)0.5) ? 1 : -1;
+        if (v2 != v) {  // integrate from the other end
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            T t;
+            t = qe[e]; qe[e] = qf[e]; qf[e] = t;
+            t = pe[e]; pe[e] = pf[e]; pf[e] = t;
+            t = ge[e]; ge[e] = gf[e]; gf[e] = t;
+          }
+        }
+        v = v2;
+        l = 0;
+        continue;
+      }
     }
-    // dual averaging (generic_nuts.rs:882-924)
+
+    // --- the transition is complete: dual averaging (generic_nuts.rs:882-924)
+    const long long m = a.m0 + s + 1;
     T eta = (T)1 / (T)(m + t0c);
     h_bar = ((T)1 - eta) * h_bar + eta * (delta - alpha / (T)n_alpha);
     if (m <= a.n_discard) {
@@ -584,6 +659,8 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     }
     if (track) tr.step(q, a.trk.n0 + (unsigned long long)s + 1ull, lane, D);
     record(a.t0 + s + 1);
+    ++s;
+    starting = true;
   }
   if (track) tr.store(a.trk, c, lane, D);
   if (a.mass_mode) {

@@ -22,8 +22,6 @@
 // their own control flow. The per-level stack of stored left subtrees lives in
 // global memory laid out [level][field][chain][coordinate]; every lane only
 // ever reads back what it wrote itself, so no cross-lane ordering is needed.
-#include <cstdlib>
-
 #include "nuts_device.h"
 #include "gm_jit.h"
 #include "gm_layouts.h"
@@ -177,6 +175,10 @@ int nuts_init_state(NutsState* ns, gm_dtype dt, long long C, int D, int max_dept
   if (e == hipSuccess) e = hipMalloc((void**)&ns->n_leapfrog, C * sizeof(long long));
   if (e == hipSuccess && max_depth > 0)
     e = hipMalloc(&ns->stk_vec, (size_t)max_depth * 3 * C * D * esz);
+  // per-chain scalars of the HBM stack levels: [max_depth][C]
+  if (e == hipSuccess && max_depth > 0) e = hipMalloc(&ns->stk_alpha, (size_t)max_depth * C * esz);
+  if (e == hipSuccess && max_depth > 0) e = hipMalloc((void**)&ns->stk_n, (size_t)max_depth * C * sizeof(int));
+  if (e == hipSuccess && max_depth > 0) e = hipMalloc((void**)&ns->stk_na, (size_t)max_depth * C * sizeof(int));
   if (e != hipSuccess) {
     set_error(std::string("NUTS state allocation failed: ") + hipGetErrorString(e));
     return GM_ENOMEM;
@@ -305,23 +307,6 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
              std::vector<hipEvent_t>& evs, double* ms, long long* launches, const TrackLaunch* trk,
              const StepHook* hook) {
   const size_t esz = dt == GM_F32 ? 4 : 8;
-  // scalar stack is per lane; (re)size for the current layout
-  const long long lanes_total = C * lay.lanes;
-  if (ns.stk_lanes != lanes_total && ns.max_depth > 0) {
-    ffree(ns.stk_alpha);
-    ffree(ns.stk_n);
-    ffree(ns.stk_na);
-    ns.stk_alpha = nullptr;
-    ns.stk_n = ns.stk_na = nullptr;
-    hipError_t e = hipMalloc(&ns.stk_alpha, (size_t)ns.max_depth * lanes_total * esz);
-    if (e == hipSuccess) e = hipMalloc((void**)&ns.stk_n, (size_t)ns.max_depth * lanes_total * sizeof(int));
-    if (e == hipSuccess) e = hipMalloc((void**)&ns.stk_na, (size_t)ns.max_depth * lanes_total * sizeof(int));
-    if (e != hipSuccess) {
-      set_error("NUTS stack allocation failed");
-      return GM_ENOMEM;
-    }
-    ns.stk_lanes = lanes_total;
-  }
   // progress == 2: NUTS::step (nuts.rs:431-433 -> generic_nuts.rs:755-925):
   // transitions that continue the chain state without init_chain_state, the
   // adaptation counter running on against the last run's n_discard, nothing
@@ -395,15 +380,16 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
   }
   int pending_refind = 0;
   uint64_t refind_step = 0;
-  // GM_NUTS_LDS_LEVELS caps the LDS stack levels (tests cover both homes)
-  const char* cap_env = getenv("GM_NUTS_LDS_LEVELS");
-  const long long lds_cap = cap_env ? atoll(cap_env) : -1;
-  int ncu = 256;
+  const long long lds_cap = ns.lds_levels_cap;  // gm_nuts_set_lds_levels (-1: as many as fit)
+  int ncu = 256, lds_max = 64 * 1024;
   {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
       ncu = 256;
+    if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess ||
+        lds_max < 1)
+      lds_max = 64 * 1024;
   }
   for (long long li = 0; li < n_launch; ++li) {
     const long long start = seg_start[li], nst = seg_len[li];
@@ -458,15 +444,16 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     }
     hipEventRecord(evs[2 * li], st);
     // LDS: the target's staging area (tgl bytes), then as many subtree-stack
-    // levels as fit without costing occupancy (<= 4 blocks of 4 waves per CU
-    // by VGPRs); returns the dynamic LDS size and sets a.lds_*
-    auto size_lds = [&](unsigned blocks, size_t tgl, int E, size_t tsz) -> size_t {
+    // levels as fit in the CU's 160 KiB shared by the grid's blocks per CU
+    // (at most 4: the kernel's VGPRs allow no more); returns the dynamic LDS
+    // size and sets a.lds_*
+    auto size_lds = [&](unsigned blocks, size_t tgl, int LPC, int E, size_t tsz) -> size_t {
       tgl = (tgl + 15) / 16 * 16;
-      const size_t per_level = (size_t)3 * 256 * E * tsz + (size_t)256 * (tsz + 8);
+      const size_t per_level = (size_t)3 * 256 * E * tsz + (size_t)(256 / LPC) * (tsz + 8);
       long long bpc = ((long long)blocks + ncu - 1) / ncu;
       bpc = bpc < 1 ? 1 : bpc > 4 ? 4 : bpc;
       size_t budget = (size_t)(160 * 1024) / (size_t)bpc - 1024;
-      if (budget > 64 * 1024) budget = 64 * 1024;
+      if (budget > (size_t)lds_max) budget = (size_t)lds_max;
       long long kl = budget > tgl ? (long long)((budget - tgl) / per_level) : 0;
       if (kl > a.max_depth) kl = a.max_depth;
       if (lds_cap >= 0 && kl > lds_cap) kl = lds_cap;
@@ -477,7 +464,7 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     hipError_t e;
     if (tg.kind == GM_TARGET_CUSTOM) {  // user target, runtime-compiled (gm_jit.cpp)
       const unsigned blocks = (unsigned)((C + 255) / 256);
-      const size_t lds = size_lds(blocks, 0, D, esz);
+      const size_t lds = size_lds(blocks, 0, 1, D, esz);
       UserTargetArg ut{tg.params, tg.D};
       void* args[] = {&a, &ut};
       e = jit_launch(JIT_NUTS, dt, tg, blocks, 256, lds, st, args);
@@ -485,7 +472,7 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
       e = dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
         const long long threads = C * LPC;
         const unsigned blocks = (unsigned)((threads + 255) / 256);
-        const size_t lds = size_lds(blocks, t.template lds_bytes<LPC, E>(), E, sizeof(T));
+        const size_t lds = size_lds(blocks, t.template lds_bytes<LPC, E>(), LPC, E, sizeof(T));
         hipLaunchKernelGGL((nuts_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), lds, st, a, t);
         return hipGetLastError();
       });

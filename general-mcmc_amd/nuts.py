@@ -97,6 +97,12 @@ class NUTS(Sampler):
         """nuts.rs:299-304 / generic_nuts.rs:550-556."""
         return self._seed(seed)
 
+    def set_lds_levels(self, levels: int):
+        """Subtree-stack levels kept in LDS (-1: as many as fit); the rest in
+        HBM. Identical results either way."""
+        _lib.check(self._lib.gm_nuts_set_lds_levels(self._h, int(levels)))
+        return self
+
     def step_sizes(self) -> tuple[np.ndarray, np.ndarray]:
         """Per-chain (epsilon, epsilon_bar)."""
         eps = np.empty(self.n_chains, dtype=np.float64)

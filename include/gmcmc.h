@@ -216,6 +216,12 @@ int gm_nuts_set_mass_adaptation(gm_sampler* s, int32_t mode, int64_t start_buffe
 /* The current metric: mode, per-chain kind [C] (0 identity, 1 diagonal,
  * 2 dense), diagonal inverse and sqrt [C][dim], dense inverse and Cholesky
  * factor [C][dim][dim] (mode 2). Any output may be NULL. */
+/* Where a NUTS sampler keeps the levels of its subtree stack (the stored
+ * left siblings of build_tree's recursion): the first `levels` in LDS, deeper
+ * ones in HBM; -1 (the default) puts as many in LDS as fit next to the
+ * target's staging area. Results are identical for every value. */
+int gm_nuts_set_lds_levels(gm_sampler* s, int32_t levels);
+
 int gm_nuts_get_mass(gm_sampler* s, int32_t* mode, int32_t* kind, void* dinv, void* dsqrt, void* minv,
                      void* mchol);
 
@@ -225,12 +231,6 @@ int gm_nuts_get_mass(gm_sampler* s, int32_t* mode, int32_t* kind, void* dinv, vo
  * butterfly over the lanes, which fixes the floating-point summation order. */
 int gm_sampler_layout(gm_sampler* s, int32_t* lanes, int32_t* elems);
 int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems);
-
-/* HMC with a 64-lane layout (lanes == 64): chains sharing one wavefront,
- * each lane holding the same coordinates of each (0 = automatic, 1, 2). Two
- * chains per wave issue two independent instruction streams per wave (more
- * latency hidden at low occupancy); samples are bit-identical either way. */
-int gm_sampler_set_chains_per_wave(gm_sampler* s, int32_t chains_per_wave);
 
 /* Device time (ms) of the sampling kernels launched by the last run, and the
  * number of launches (HIP events on the sampler's stream). */

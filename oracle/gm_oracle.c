@@ -262,6 +262,37 @@ static float uniform_oc_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t
   return unif_oc_f(x[step % 4]);
 }
 
+/* NUTS per-transition draws (stream spec v3). One Philox
+ * block per (chain, transition st):
+ *   x = philox({0, chain, st_lo, TAG_NUTS_EXP | st_hi << 8}, seed)
+ * words 0,1: the transition's 64-bit stream key K (x0 | x1 << 32);
+ * words 2,3: the slice variable's Exp1 = -ln u, u in (0,1] (f64 from (x2, x3),
+ * f32 from x2). Every other scalar draw of the transition is
+ *   h(K, idx) = mix64(K + (idx + 1) * 0x9E3779B97F4A7C15)
+ * (the SplitMix64 finalizer over a Weyl sequence): doubling j's direction
+ * uniform idx 2j, its top-level accept uniform idx 2j + 1, merge m (recursion
+ * post-order) idx 64 + m; uniforms in [0,1): f64 (h >> 11) 2^-53, f32 (h >> 40)
+ * 2^-24. One Philox per transition instead of one per draw. */
+uint64_t or_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+uint64_t or_nuts_key(uint64_t seed, uint32_t chain, uint64_t st, uint32_t w[4]) {
+  block(seed, chain, st, TAG_NUTS_EXP, 0u, w);
+  return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+}
+double or_nuts_u_d(uint64_t key, uint32_t idx) {
+  const uint64_t h = or_mix64(key + (uint64_t)(idx + 1u) * 0x9E3779B97F4A7C15ull);
+  return (double)(h >> 11) * 1.1102230246251565e-16;
+}
+float or_nuts_u_f(uint64_t key, uint32_t idx) {
+  const uint64_t h = or_mix64(key + (uint64_t)(idx + 1u) * 0x9E3779B97F4A7C15ull);
+  return (float)(uint32_t)(h >> 40) * 5.9604644775390625e-08f;
+}
+static double nuts_exp1_d(const uint32_t w[4]) { return -or_log_d(unif_oc_d(w[2], w[3])); }
+static float nuts_exp1_f(const uint32_t w[4]) { return -or_log_f(unif_oc_f(w[2])); }
+
 /* ===================== threading helper ===================== */
 typedef struct {
   void (*fn)(void* ctx, int64_t c0, int64_t c1);
@@ -306,6 +337,8 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #define NORMAL or_normal_d
 #define UNIF_CO or_uniform_co_d
 #define UNIF_OC uniform_oc_d
+#define NUTS_U or_nuts_u_d
+#define NUTS_EXP1 nuts_exp1_d
 #define MACH_EPS 2.220446049250313e-16
 #include "gm_oracle_t.inc"
 #undef T
@@ -317,6 +350,8 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #undef NORMAL
 #undef UNIF_CO
 #undef UNIF_OC
+#undef NUTS_U
+#undef NUTS_EXP1
 #undef MACH_EPS
 
 #define T float
@@ -328,6 +363,8 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #define NORMAL or_normal_f
 #define UNIF_CO or_uniform_co_f
 #define UNIF_OC uniform_oc_f
+#define NUTS_U or_nuts_u_f
+#define NUTS_EXP1 nuts_exp1_f
 #define MACH_EPS 1.1920928955078125e-07f
 #include "gm_oracle_t.inc"
 #undef T
@@ -657,6 +694,8 @@ void or_build_tree_d(const or_target* t, int lanes, int elems, const double* q, 
   memset(&cx, 0, sizeof(cx));
   cx.t = t; cx.lanes = lanes; cx.elems = elems; cx.D = D;
   cx.seed = seed; cx.cid = chain; cx.step = step;
+  uint32_t kw[4];
+  cx.key = or_nuts_key(seed, chain, step, kw);
   for (int k = 0; k < 32; ++k) tree_alloc_d(&cx.ws[k], D);
   cx.tmpv = (double*)malloc(sizeof(double) * D);
   cx.tmpv2 = (double*)malloc(sizeof(double) * D);

@@ -55,6 +55,12 @@ float or_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, ui
 double or_uniform_co_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
 float or_uniform_co_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
 
+/* NUTS per-transition stream (spec v3): key block and the hashed draws */
+uint64_t or_mix64(uint64_t z);
+uint64_t or_nuts_key(uint64_t seed, uint32_t chain, uint64_t st, uint32_t w[4]);
+double or_nuts_u_d(uint64_t key, uint32_t idx);
+float or_nuts_u_f(uint64_t key, uint32_t idx);
+
 /* ---- targets ---- */
 double or_logp_grad_d(const or_target* t, int lanes, int elems, const double* x, double* g);
 float or_logp_grad_f(const or_target* t, int lanes, int elems, const float* x, float* g);

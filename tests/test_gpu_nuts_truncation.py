@@ -13,13 +13,11 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("nd", [5, 10, 40])
-@pytest.mark.parametrize("lds_levels", [None, "0", "1"])  # subtree stack in LDS / HBM / split
-def test_step_sizes_match_oracle(gm, oracle, dtype, nd, lds_levels, monkeypatch):
-    if lds_levels is not None:
-        monkeypatch.setenv("GM_NUTS_LDS_LEVELS", lds_levels)
+@pytest.mark.parametrize("lds_levels", [-1, 0, 1])  # subtree stack in LDS / HBM / split
+def test_step_sizes_match_oracle(gm, oracle, dtype, nd, lds_levels):
     t = gm.DenseGaussian(np.zeros(4), np.diag([0.04, 1.0, 4.0, 0.5]))
     x0 = gm.init_with_seed(24, 4, 3, dtype)
-    s = gm.NUTS(t, x0, 0.8, dtype=dtype).set_seed(11)
+    s = gm.NUTS(t, x0, 0.8, dtype=dtype).set_seed(11).set_lds_levels(lds_levels)
     lanes, elems = s.layout()
     out = s.run(3, nd)
     st = oracle.nuts_state(24, dtype)

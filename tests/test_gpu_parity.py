@@ -109,10 +109,8 @@ def test_mh_samples_bitwise(gm, oracle, dtype, dim, lay):
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("dim,lay", [(2, (2, 1)), (5, (8, 1)), (32, (32, 1)), (32, (16, 2))])
 @pytest.mark.parametrize("progress", [False, True])
-@pytest.mark.parametrize("lds_levels", [None, "0", "2"])  # subtree stack in LDS / HBM / split
-def test_nuts_samples_bitwise(gm, oracle, dtype, dim, lay, progress, lds_levels, monkeypatch):
-    if lds_levels is not None:
-        monkeypatch.setenv("GM_NUTS_LDS_LEVELS", lds_levels)
+@pytest.mark.parametrize("lds_levels", [-1, 0, 2])  # subtree stack in LDS / HBM / split
+def test_nuts_samples_bitwise(gm, oracle, dtype, dim, lay, progress, lds_levels):
     n_chains = 12
     x0 = start(gm, n_chains, dim, dtype, 0.5)
     for name, t in targets(gm, dim):
@@ -120,6 +118,7 @@ def test_nuts_samples_bitwise(gm, oracle, dtype, dim, lay, progress, lds_levels,
             continue  # deep trees on high-dim Rosenbrock: slow oracle, same code path
         s = gm.NUTS(t, x0, 0.8, dtype=dtype, max_depth=6).set_seed(9)
         s.set_layout(*lay)
+        s.set_lds_levels(lds_levels)
         s.set_steps_per_launch(3)
         n_collect, n_discard = 5, 4
         if progress:
@@ -160,24 +159,3 @@ def test_split_rhat_ess_matches_oracle(gm, oracle, shape, dtype):
     np.testing.assert_allclose(r, orr, atol=1e-3)  # north-star tolerance: R-hat within 1e-3
     np.testing.assert_allclose(e, oe, rtol=1e-3)
 
-
-@pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("dim,lay", [(33, (64, 1)), (64, (64, 1)), (100, (64, 2)), (256, (64, 4))])
-@pytest.mark.parametrize("n_chains", [24, 25])  # an odd count leaves one wave a single chain
-def test_hmc_two_chains_per_wave_bitwise(gm, oracle, dtype, dim, lay, n_chains):
-    """hmc_kernel_cw (two chains per wavefront) == the oracle == hmc_kernel."""
-    L, eps = 7, 0.01
-    x0 = start(gm, n_chains, dim, dtype)
-    for name, t in targets(gm, dim):
-        outs = []
-        for cw in (2, 1):
-            s = gm.HMC(t, x0, eps, L, dtype=dtype).set_seed(11)
-            s.set_layout(*lay).set_chains_per_wave(cw)
-            s.set_steps_per_launch(5)
-            outs.append((s.run(6, 3), s.positions(), s.accept_counts()))
-            s.close()
-        q, samples, acc = oracle.hmc_run(Target.from_product(t, dim), x0, eps, L, 11, 0, 9, 3, *lay)
-        np.testing.assert_array_equal(outs[0][0], samples.transpose(1, 0, 2), err_msg=name)
-        np.testing.assert_array_equal(outs[0][1], q, err_msg=name)
-        np.testing.assert_array_equal(outs[0][2], acc, err_msg=name)
-        np.testing.assert_array_equal(outs[0][0], outs[1][0], err_msg=name)

@@ -58,3 +58,15 @@ def test_normal_stream_moments(oracle, sfx):
     assert abs(z.std() - 1) < 0.02
     assert abs(np.mean(z ** 3)) < 0.06
     assert abs(np.mean(z ** 4) - 3) < 0.15
+
+
+def test_nuts_stream_mix64_splitmix_kat(oracle):
+    """The NUTS per-transition draws hash K + (idx + 1) * 0x9E3779B97F4A7C15
+    with the SplitMix64 finalizer: K = 1234567 reproduces the published
+    SplitMix64 sequence (Vigna's splitmix64.c test values)."""
+    import ctypes as C
+    lib = oracle.lib
+    lib.or_mix64.restype = C.c_uint64
+    lib.or_mix64.argtypes = [C.c_uint64]
+    seq = [lib.or_mix64((1234567 + (i + 1) * 0x9E3779B97F4A7C15) & (2**64 - 1)) for i in range(3)]
+    assert seq == [6457827717110365317, 3203168211198807973, 9817491932198370423]

@@ -22,14 +22,12 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--warm-collect", action="store_true")
 ap.add_argument("--repeat", type=int, default=8)
-ap.add_argument("--cw", type=int, default=0)
 a = ap.parse_args()
 lib = _lib.load()
 _lib.check(lib.gm_set_device(0))
 lib = _lib.require_gpu()
 x0 = gm.init_with_seed(4096, 64, 42, np.float64).astype(np.float32)
 s = gm.HMC(gm.RosenbrockND(), x0, 0.01, 50).set_seed(42)
-s.set_chains_per_wave(a.cw)
 s.reserve(a.steps)
 if a.warm_collect:
     s.run_positions(a.warmup, 0)
@@ -43,7 +41,7 @@ for i in range(1 + a.repeat):
     _lib.check(lib.gm_device_synchronize())
     walls.append((time.perf_counter() - t0) * 1e6)
     kerns.append(s.last_run_stats()[0] * 1e3)
-print(json.dumps({"lib": os.environ.get("GMCMC_LIB", "default"), "warm_collect": a.warm_collect, "cw": a.cw,
+print(json.dumps({"lib": os.environ.get("GMCMC_LIB", "default"), "warm_collect": a.warm_collect,
                   "first_wall_us": walls[0], "first_kernel_us": kerns[0],
                   "repeat_wall_us_median": float(np.median(walls[1:])),
                   "repeat_kernel_us_median": float(np.median(kerns[1:])),

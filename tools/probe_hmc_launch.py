@@ -26,7 +26,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="")
     ap.add_argument("--reps", type=int, default=30)
-    ap.add_argument("--cw", type=int, default=0, help="chains per wave (0 automatic)")
     ap.add_argument("--chains", type=int, default=4096)
     ap.add_argument("--quick", action="store_true", help="kernel-vs-K fit only")
     a = ap.parse_args()
@@ -34,7 +33,6 @@ def main():
     _lib.check(lib.gm_set_device(0))
     C, D, L = a.chains, 64, 50
     s = gm.HMC(gm.RosenbrockND(), gm.init_with_seed(C, D, 42, np.float64).astype(np.float32), 0.01, L).set_seed(42)
-    s.set_chains_per_wave(a.cw)
     s.reserve(200)
     s.run_positions(0, 5)
     res = {"shape": f"{C}x{D} f32 L={L}"}
@@ -52,7 +50,6 @@ def main():
     slope, icpt = np.polyfit(x, y, 1)
     res["fit_us_per_transition"] = float(slope)
     res["fit_us_per_launch_fixed"] = float(icpt)
-    res["chains_per_wave"] = a.cw
     if a.quick:
         print(json.dumps(res))
         if a.out:
@@ -93,7 +90,6 @@ def main():
     res["idle_device_sync_us"] = med(sy)
     # L = 0: the per-transition cost outside the leapfrog loop
     s0 = gm.HMC(gm.RosenbrockND(), gm.init_with_seed(C, D, 42, np.float64).astype(np.float32), 0.01, 0).set_seed(1)
-    s0.set_chains_per_wave(a.cw)
     s0.reserve(200)
     s0.run_positions(0, 5)
     l0 = {}
@@ -102,7 +98,6 @@ def main():
             s0.run_positions(k, 0)
             l0.setdefault(k, []).append(s0.last_run_stats()[0] * 1e3)
     res["L0_kernel_us_by_K"] = {k: med(v) for k, v in l0.items()}
-    res["chains_per_wave"] = a.cw
     res["env"] = {k: os.environ.get(k) for k in ("GM_SYNC_SPIN", "HIP_FORCE_DEV_KERNARG")}
     print(json.dumps(res, indent=1))
     if a.out:
