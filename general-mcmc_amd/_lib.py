@@ -128,6 +128,9 @@ SIGNATURES = {
     "gm_bv_energy_neg": (_ip, [_ip, _i64, _vp, _vp]),
     "gm_bv_energy_ln": (_ip, [_ip, _i64, _vp, _vp]),
     "gm_bv_accept_mask": (_ip, [_ip, _i64, _vp, _vp, _vp]),
+    "gm_bv_scale_assign": (_ip, [_ip, _i64, _vp, _dbl]),
+    "gm_bv_fill": (_ip, [_ip, _i64, _vp, _dbl]),
+    "gm_bv_dot": (_ip, [_ip, _i64, _vp, _vp, C.POINTER(_dbl)]),
     "gm_bv_target_create": (_ip, [C.POINTER(gm_target), _ip, C.POINTER(_vp)]),
     "gm_bv_logp_and_grad": (_ip, [_vp, _i64, _vp, _vp, _vp]),
     "gm_bv_target_destroy": (_ip, [_vp]),
@@ -148,6 +151,8 @@ def load(path: str | None = None) -> C.CDLL:
                                  "(no CPU fallback exists)")
     lib = C.CDLL(p)
     for name, (res, args) in SIGNATURES.items():
+        if "GMCMC_LIB" in os.environ and not hasattr(lib, name):
+            continue  # an A/B build of an earlier tree may predate an entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -113,6 +113,24 @@ def add_scaled_assign(x: DeviceMatrix, other: DeviceMatrix, alpha: float) -> Non
     _lib.check(x.lib.gm_bv_add_scaled_assign(x.code, n, _vp(x), _vp(other), float(alpha)))
 
 
+def scale_assign(x: DeviceMatrix, alpha: float) -> None:
+    """x = x * alpha (EuclideanVector::scale_assign, euclidean.rs:396-398)."""
+    _lib.check(x.lib.gm_bv_scale_assign(x.code, int(np.prod(x.shape)), _vp(x), float(alpha)))
+
+
+def fill(x: DeviceMatrix, value: float = 0.0) -> None:
+    """Every element = value (fill_zero / zeros_like, euclidean.rs:22-26)."""
+    _lib.check(x.lib.gm_bv_fill(x.code, int(np.prod(x.shape)), _vp(x), float(value)))
+
+
+def dot(a: DeviceMatrix, b: DeviceMatrix) -> float:
+    """Sum of a*b over every element (EuclideanVector::dot, euclidean.rs:400-403)."""
+    _same(a, b)
+    out = C.c_double()
+    _lib.check(a.lib.gm_bv_dot(a.code, int(np.prod(a.shape)), _vp(a), _vp(b), C.byref(out)))
+    return out.value
+
+
 def fill_random_normal(x: DeviceMatrix, seed: int, step: int, chain_offset: int = 0) -> None:
     """N(0, 1) momentum draws of transition `step` (euclidean.rs:484-496)."""
     _lib.check(x.lib.gm_bv_fill_random_normal(x.code, x.n_chains, x.dim, _vp(x), seed, chain_offset, step))

@@ -62,6 +62,35 @@ __global__ void bv_axpy_kernel(long long n, T* __restrict__ x, const T* __restri
   if (k < n) x[k] = x[k] + o[k] * alpha;
 }
 
+// scale_assign (euclidean.rs:396-398): x = x * alpha; fill_zero (:370-374) as a fill
+template <class T>
+__global__ void bv_scale_kernel(long long n, T* __restrict__ x, T alpha) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) x[k] = x[k] * alpha;
+}
+template <class T>
+__global__ void bv_fill_kernel(long long n, T* __restrict__ x, T v) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) x[k] = v;
+}
+// dot (euclidean.rs:400-403): sum over every element of a*b, one block:
+// thread t sums elements t, t+1024, ... left to right, then a fixed pairwise
+// tree over the 1024 partials (deterministic, summed in T)
+template <class T>
+__global__ __launch_bounds__(1024) void bv_dot_kernel(long long n, const T* __restrict__ a, const T* __restrict__ b,
+                                                      double* __restrict__ out) {
+  __shared__ T part[1024];
+  T s = (T)0;
+  for (long long k = threadIdx.x; k < n; k += 1024) s = s + a[k] * b[k];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] = part[threadIdx.x] + part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (double)part[0];
+}
+
 // fill_random_normal (euclidean.rs:484-496): N(0,1) from the momentum stream
 template <class T>
 __global__ void bv_normal_kernel(long long C, int D, T* __restrict__ out, uint64_t seed,
@@ -127,6 +156,28 @@ hipError_t launch_bv_axpy(gm_dtype dt, long long n, void* x, const void* o, doub
   else
     hipLaunchKernelGGL(bv_axpy_kernel<double>, dim3(grid_for(n)), dim3(256), 0, st, n, (double*)x,
                        (const double*)o, alpha);
+  return hipGetLastError();
+}
+hipError_t launch_bv_scale(gm_dtype dt, long long n, void* x, double alpha, hipStream_t st) {
+  if (dt == GM_F32)
+    hipLaunchKernelGGL(bv_scale_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, n, (float*)x, (float)alpha);
+  else
+    hipLaunchKernelGGL(bv_scale_kernel<double>, dim3(grid_for(n)), dim3(256), 0, st, n, (double*)x, alpha);
+  return hipGetLastError();
+}
+hipError_t launch_bv_fill(gm_dtype dt, long long n, void* x, double v, hipStream_t st) {
+  if (dt == GM_F32)
+    hipLaunchKernelGGL(bv_fill_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, n, (float*)x, (float)v);
+  else
+    hipLaunchKernelGGL(bv_fill_kernel<double>, dim3(grid_for(n)), dim3(256), 0, st, n, (double*)x, v);
+  return hipGetLastError();
+}
+hipError_t launch_bv_dot(gm_dtype dt, long long n, const void* a, const void* b, double* out, hipStream_t st) {
+  if (dt == GM_F32)
+    hipLaunchKernelGGL(bv_dot_kernel<float>, dim3(1), dim3(1024), 0, st, n, (const float*)a, (const float*)b, out);
+  else
+    hipLaunchKernelGGL(bv_dot_kernel<double>, dim3(1), dim3(1024), 0, st, n, (const double*)a, (const double*)b,
+                       out);
   return hipGetLastError();
 }
 hipError_t launch_bv_normal(gm_dtype dt, long long C, int D, void* out, uint64_t seed, uint32_t off,

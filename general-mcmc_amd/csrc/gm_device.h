@@ -539,6 +539,12 @@ template <class T, int LPC, int E> struct GaussLane {
       const int i = lane * E + e;
       d[e] = (i < D) ? x[e] - mur[e] : (T)0;
     }
+#ifdef GM_AB_NOGEMV  // A/B timing only (wrong results): w = d, no product
+    if (true) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) w[e] = d[e];
+    } else
+#endif
     if (sprec) {
       constexpr int S = LPC * E;
       // the previous evaluation's broadcast reads are done before d is replaced

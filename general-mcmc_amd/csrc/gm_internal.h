@@ -36,27 +36,23 @@ bool wide_layout_supported(int lanes, int elems, gm_dtype dt);
 constexpr int GM_WIDE_MAX_DIM = 16384;
 Layout default_layout(int D, gm_dtype dt, int kind);
 
-// Events a launcher records around its kernel (either may be null): the AOT
-// kernels carry them in their dispatch (hipExtLaunchKernel), so timing a run
-// adds no packets of its own to the stream.
+// Events a launcher records around its kernel (either may be null).
 struct LaunchEvents {
   hipEvent_t start = nullptr, stop = nullptr;
 };
 
-// An AOT kernel launch carrying its timing events in the dispatch.
+// An AOT kernel launch between its timing events (event records on the
+// stream; hipExtLaunchKernel's in-dispatch events measured 8-14 us slower per
+// call on the host, profiles/r02/launch_ab.json).
 template <class... A>
 hipError_t launch_timed(void (*k)(A...), dim3 grid, dim3 block, size_t lds, hipStream_t st, LaunchEvents ev,
                         A... args) {
-#ifdef GM_AB_EVREC  // A/B builds only: separate event-record packets
-  if (ev.start) hipEventRecord(ev.start, st);
+  hipError_t e = ev.start ? hipEventRecord(ev.start, st) : hipSuccess;
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, grid, block, lds, st, args...);
-  if (ev.stop) hipEventRecord(ev.stop, st);
-  return hipGetLastError();
-#else
-  void* ptrs[] = {(void*)&args...};
-  const hipError_t e = hipExtLaunchKernel((const void*)k, grid, block, ptrs, lds, st, ev.start, ev.stop, 0);
-  return e != hipSuccess ? e : hipGetLastError();
-#endif
+  e = hipGetLastError();
+  if (e == hipSuccess && ev.stop) e = hipEventRecord(ev.stop, st);
+  return e;
 }
 // The same events around a launch path that goes through another API (the
 // runtime-compiled user-target kernels).
@@ -104,6 +100,9 @@ hipError_t launch_bv_kinetic(gm_dtype dt, const Layout& lay, long long C, int D,
 hipError_t launch_bv_masked_assign(gm_dtype dt, long long C, int D, void* x, const void* o,
                                    const uint8_t* mask, hipStream_t st);
 hipError_t launch_bv_axpy(gm_dtype dt, long long n, void* x, const void* o, double alpha, hipStream_t st);
+hipError_t launch_bv_scale(gm_dtype dt, long long n, void* x, double alpha, hipStream_t st);
+hipError_t launch_bv_fill(gm_dtype dt, long long n, void* x, double v, hipStream_t st);
+hipError_t launch_bv_dot(gm_dtype dt, long long n, const void* a, const void* b, double* out, hipStream_t st);
 hipError_t launch_bv_normal(gm_dtype dt, long long C, int D, void* out, uint64_t seed, uint32_t off,
                             uint64_t step, uint32_t tag, hipStream_t st);
 hipError_t launch_bv_uniform(gm_dtype dt, long long C, void* out, uint64_t seed, uint32_t off, uint64_t step,

@@ -66,8 +66,10 @@ std::string program_source(JitKernel which, const char* src, int D) {
 
 std::string name_expr(JitKernel which, gm_dtype dt, int D) {
   const char* t = dt == GM_F32 ? "float" : "double";
+  // the NUTS kernel's last argument: metric handling compiled in (user
+  // targets run with or without mass-matrix adaptation from one module)
   return std::string("gm::") + kKernelName[which] + "<" + t + ", 1, " + std::to_string(D) +
-         ", gm::UserTarget<" + t + "> >";
+         ", gm::UserTarget<" + t + ">" + (which == JIT_NUTS ? ", true" : "") + " >";
 }
 
 // compile; on success fills code and the lowered kernel name

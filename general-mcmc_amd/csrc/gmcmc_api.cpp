@@ -304,11 +304,10 @@ int gm_device_count(int* count) {
 }
 
 int gm_set_device(int device) {
+#ifdef GM_AB_SPIN  // A/B builds only: spinning host waits (set before the device is initialised)
+  hipSetDeviceFlags(hipDeviceScheduleSpin);
+#endif
   GM_HIP(hipSetDevice(device));
-  // GM_SYNC_SPIN=1: host waits spin instead of yielding (lower completion
-  // latency for short synchronous runs, at the cost of a busy host core)
-  const char* spin = getenv("GM_SYNC_SPIN");
-  if (spin && atoi(spin) == 1) hipSetDeviceFlags(hipDeviceScheduleSpin);
   return GM_OK;
 }
 
@@ -608,22 +607,6 @@ static hipError_t use_device(int dev) {
   return e;
 }
 
-// The end of a run: poll the stop event (the run's last launch completing)
-// instead of a blocking stream wait, whose wake-up after an idle stretch
-// costs microseconds on every run; then drain the stream.
-static hipError_t wait_event(hipEvent_t ev, hipStream_t st) {
-#ifdef GM_AB_BLOCKSYNC  // A/B builds only
-  (void)ev;
-  return hipStreamSynchronize(st);
-#else
-  hipError_t e;
-  while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
-  }
-  if (e != hipSuccess) return e;
-  return hipStreamSynchronize(st);
-#endif
-}
-
 // One event pair per run (before the first launch, after the last): the
 // device time of the run's launches, read back after the run's stream
 // synchronize.
@@ -725,7 +708,7 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
   }
   s->step += total;
   s->total_steps += total;
-  GM_HIP(wait_event(s->evs[1], s->stream));
+  GM_HIP(hipStreamSynchronize(s->stream));
   float t = 0;
   GM_HIP(hipEventElapsedTime(&t, s->evs[0], s->evs[1]));
   s->last_ms = t;
@@ -1165,6 +1148,43 @@ size_t state_bytes(gm_sampler* s) { return parts_bytes(state_parts_for(s, s->kin
 }  // namespace
 
 extern "C" {
+
+#ifdef GM_HOST_TEST
+// Host-only test hooks, compiled into the AddressSanitizer build of the host
+// code only (tools/asan, tests/test_asan_host.py): a sampler shell with no
+// device memory, and a well-formed state header for it, so that blob parsing
+// and argument validation run under ASan on a machine without a GPU.
+gm_sampler* gm_test_sampler(int kind, int dtype, long long C, int D, int mass_mode) {
+  gm_sampler* s = new gm_sampler();
+  s->kind = kind;
+  s->dt = (gm_dtype)dtype;
+  s->esz = dtype == GM_F32 ? 4 : 8;
+  s->C = C;
+  s->D = D;
+  s->eps = 0.01;
+  s->L = 5;
+  s->nuts.mass_mode = kind == K_NUTS ? mass_mode : 0;
+  return s;
+}
+void gm_test_sampler_free(gm_sampler* s) { delete s; }
+uint64_t gm_test_state_header(gm_sampler* s, void* out) {
+  StateHeader h;
+  memset(&h, 0, sizeof(h));
+  memcpy(h.magic, "GMCMCST2", 8);
+  h.kind = s->kind;
+  h.dtype = s->dt;
+  h.C = s->C;
+  h.D = s->D;
+  h.eps = s->eps;
+  h.L = s->L;
+  h.prop_std = s->prop_std;
+  h.target_accept = s->target_accept;
+  h.max_depth = s->max_depth;
+  h.mass_mode = s->kind == K_NUTS ? s->nuts.mass_mode : 0;
+  memcpy(out, &h, sizeof(h));
+  return sizeof(h);
+}
+#endif
 
 int gm_state_size(gm_sampler* s, uint64_t* bytes) {
   GM_REQ(s && bytes, "bad arguments");

@@ -84,6 +84,28 @@ int gm_bv_add_scaled_assign(gm_dtype dt, int64_t n, void* x, const void* o, doub
   BV_REQ(x && o, "NULL pointer");
   return bv_status(launch_bv_axpy(dt, n, x, o, alpha, nullptr), "add_scaled_assign");
 }
+int gm_bv_scale_assign(gm_dtype dt, int64_t n, void* x, double alpha) {
+  BV_REQ(dtype_ok(dt) && n >= 0 && (x || n == 0), "bad arguments");
+  if (n == 0) return GM_OK;
+  return bv_status(launch_bv_scale(dt, n, x, alpha, nullptr), "scale_assign");
+}
+int gm_bv_fill(gm_dtype dt, int64_t n, void* x, double value) {
+  BV_REQ(dtype_ok(dt) && n >= 0 && (x || n == 0), "bad arguments");
+  if (n == 0) return GM_OK;
+  return bv_status(launch_bv_fill(dt, n, x, value, nullptr), "fill");
+}
+int gm_bv_dot(gm_dtype dt, int64_t n, const void* a, const void* b, double* out) {
+  BV_REQ(dtype_ok(dt) && n >= 0 && out && ((a && b) || n == 0), "bad arguments");
+  static thread_local double* dres = nullptr;
+  if (!dres && hipMalloc(&dres, sizeof(double)) != hipSuccess) {
+    dres = nullptr;
+    set_error("device allocation failed in dot");
+    return GM_ENOMEM;
+  }
+  int rc = bv_status(launch_bv_dot(dt, n, a, b, dres, nullptr), "dot");
+  if (rc) return rc;
+  return bv_status(hipMemcpy(out, dres, sizeof(double), hipMemcpyDeviceToHost), "dot copy");
+}
 int gm_bv_fill_random_normal(gm_dtype dt, int64_t C, int64_t D, void* out, uint64_t seed,
                              uint32_t chain_offset, uint64_t step) {
   BV_REQ(dtype_ok(dt), "bad dtype");

@@ -20,22 +20,28 @@ __device__ __forceinline__ T coord(const T (&x)[E], int j) {
   else return __shfl(mine, src, LPC);
 }
 
-// MassMatrix (generic_nuts.rs:175-304) of one chain, this lane's view
-template <class T, int E> struct MassDev {
-  int kind = 0;             // 0 identity, 1 diagonal, 2 dense
+// MassMatrix (generic_nuts.rs:175-304) of one chain, this lane's view. DYN
+// false: the identity metric known at compile time (a sampler without
+// mass-matrix adaptation), so no metric branch is ever emitted.
+template <class T, int E, bool DYN = true> struct MassDev {
+  int kind_ = 0;            // 0 identity, 1 diagonal, 2 dense
   T inv[E], sq[E];          // diagonal
   const T* minv = nullptr;  // dense [D][D]
   const T* chol = nullptr;
   int D = 0;
+  __device__ __forceinline__ int kind() const {
+    if constexpr (DYN) return kind_;
+    else return 0;
+  }
 };
 
 // inv_mul (:255-273): v = M^-1 p
-template <int LPC, int E, class T>
-__device__ __forceinline__ void inv_mul(const MassDev<T, E>& M, const T (&p)[E], T (&v)[E], int lane) {
-  if (M.kind == 1) {
+template <int LPC, int E, class T, bool DYN>
+__device__ __forceinline__ void inv_mul(const MassDev<T, E, DYN>& M, const T (&p)[E], T (&v)[E], int lane) {
+  if (M.kind() == 1) {
 #pragma unroll
     for (int e = 0; e < E; ++e) v[e] = M.inv[e] * p[e];
-  } else if (M.kind == 2) {
+  } else if (M.kind() == 2) {
     T acc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
@@ -56,12 +62,12 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E>& M, const T (&p)[E],
 }
 
 // sample_momentum (:275-303) applied to standard normals z
-template <int LPC, int E, class T>
-__device__ __forceinline__ void momentum_from(const MassDev<T, E>& M, const T (&z)[E], T (&p)[E], int lane) {
-  if (M.kind == 1) {
+template <int LPC, int E, class T, bool DYN>
+__device__ __forceinline__ void momentum_from(const MassDev<T, E, DYN>& M, const T (&z)[E], T (&p)[E], int lane) {
+  if (M.kind() == 1) {
 #pragma unroll
     for (int e = 0; e < E; ++e) p[e] = z[e] * M.sq[e];
-  } else if (M.kind == 2) {
+  } else if (M.kind() == 2) {
     T acc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
@@ -132,11 +138,11 @@ __device__ __forceinline__ bool no_uturn(const T (&qm)[E], const T (&qp)[E], con
 
 // MassMatrix::kinetic (:226-253), canonical-order sum of the per-coordinate
 // terms p*p*inv (diagonal) or p_i (M^-1 p)_i (dense)
-template <int LPC, int E, class T>
-__device__ __forceinline__ T kinetic_m(const MassDev<T, E>& M, const T (&p)[E], int lane) {
-  if (M.kind == 0) return kinetic<LPC, E>(p);
+template <int LPC, int E, class T, bool DYN>
+__device__ __forceinline__ T kinetic_m(const MassDev<T, E, DYN>& M, const T (&p)[E], int lane) {
+  if (M.kind() == 0) return kinetic<LPC, E>(p);
   T t[E];
-  if (M.kind == 1) {
+  if (M.kind() == 1) {
 #pragma unroll
     for (int e = 0; e < E; ++e) t[e] = p[e] * p[e] * M.inv[e];
   } else {
@@ -151,10 +157,10 @@ __device__ __forceinline__ T kinetic_m(const MassDev<T, E>& M, const T (&p)[E], 
 }
 
 // leapfrog_with_mass (:1396-1418): drift by M^-1 p
-template <int LPC, int E, class T, class TG>
-__device__ __forceinline__ T leapfrog_m(const TG& tg, const MassDev<T, E>& M, T (&q)[E], T (&p)[E],
+template <int LPC, int E, class T, class TG, bool DYN>
+__device__ __forceinline__ T leapfrog_m(const TG& tg, const MassDev<T, E, DYN>& M, T (&q)[E], T (&p)[E],
                                         T (&g)[E], T epsv, int lane) {
-  if (M.kind == 0) return leapfrog<LPC, E>(tg, q, p, g, epsv, lane);
+  if (M.kind() == 0) return leapfrog<LPC, E>(tg, q, p, g, epsv, lane);
   const T h = epsv * (T)0.5;
 #pragma unroll
   for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * h;
@@ -171,13 +177,13 @@ __device__ __forceinline__ T leapfrog_m(const TG& tg, const MassDev<T, E>& M, T 
 // Unreduced per-lane term of MassMatrix::kinetic (:226-253) without the
 // 0.5: sum_e p_e^2 (identity), p_e^2 inv_e (diagonal), p_e (M^-1 p)_e
 // (dense); kinetic = 0.5 * group_sum(part), the operations of kinetic_m.
-template <int LPC, int E, class T>
-__device__ __forceinline__ T kin_part_m(const MassDev<T, E>& M, const T (&p)[E], int lane) {
+template <int LPC, int E, class T, bool DYN>
+__device__ __forceinline__ T kin_part_m(const MassDev<T, E, DYN>& M, const T (&p)[E], int lane) {
   T t[E];
-  if (M.kind == 0) {
+  if (M.kind() == 0) {
 #pragma unroll
     for (int e = 0; e < E; ++e) t[e] = p[e] * p[e];
-  } else if (M.kind == 1) {
+  } else if (M.kind() == 1) {
 #pragma unroll
     for (int e = 0; e < E; ++e) t[e] = p[e] * p[e] * M.inv[e];
   } else {
@@ -192,10 +198,10 @@ __device__ __forceinline__ T kin_part_m(const MassDev<T, E>& M, const T (&p)[E],
 }
 
 // stop_criterion_with_mass (:1354-1378), the top-level U-turn
-template <int LPC, int E, class T>
-__device__ __forceinline__ bool no_uturn_m(const MassDev<T, E>& M, const T (&qm)[E], const T (&qp)[E],
+template <int LPC, int E, class T, bool DYN>
+__device__ __forceinline__ bool no_uturn_m(const MassDev<T, E, DYN>& M, const T (&qm)[E], const T (&qp)[E],
                                            const T (&pm)[E], const T (&pp)[E], int lane) {
-  if (M.kind == 0) return no_uturn<LPC, E>(qm, qp, pm, pp);
+  if (M.kind() == 0) return no_uturn<LPC, E>(qm, qp, pm, pp);
   T d[E], vm[E], vp[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) d[e] = qp[e] - qm[e];
@@ -231,8 +237,10 @@ template <> struct MachEps<float> { static constexpr float v = 1.192092895507812
 template <> struct MachEps<double> { static constexpr double v = 2.220446049250313e-16; };
 
 // find_reasonable_epsilon_with_mass (generic_nuts.rs:1025-1102), identity mass.
+// (not inlined: called once per launch at most, it would otherwise put its
+// leapfrog loops and their registers into the hot tree loop's code)
 template <int LPC, int E, class T, class TG>
-__device__ T find_reasonable_epsilon(const TG& tg, const T (&q0)[E], const T (&p0)[E], int lane, int D) {
+__device__ __attribute__((noinline)) T find_reasonable_epsilon(const TG& tg, const T (&q0)[E], const T (&p0)[E], int lane, int D) {
   const T half = (T)0.5;
   T eps = (T)1;
   T g0[E];
@@ -287,7 +295,7 @@ __device__ T find_reasonable_epsilon(const TG& tg, const T (&q0)[E], const T (&p
 // half) and ends the doubling. The trajectory ends live in registers as the
 // edge (the end being integrated, side v) and the far end; a direction change
 // swaps them.
-template <class T, int LPC, int E, class TG>
+template <class T, int LPC, int E, class TG, bool MASS>
 __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
@@ -381,12 +389,12 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long t0c = 10;
 
   // the chain's metric and warm-up statistics (generic_nuts.rs:33-359)
-  MassDev<T, E> M;
+  MassDev<T, E, MASS> M;
   M.D = D;
   int rn = 0;
   T rmean[E], rm2d[E];
-  if (a.mass_mode) {
-    M.kind = a.mkind[c];
+  if (MASS && a.mass_mode) {
+    M.kind_ = a.mkind[c];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
@@ -537,7 +545,11 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     const T joint = lp - kin;
     tn = (logu < joint) ? 1 : 0;
     ts = (logu - (T)1000) < joint;
+#ifdef GM_AB_NOEXP  // A/B timing only (wrong results)
+    ta = joint > joint0 ? (T)1 : (T)0.5;
+#else
     ta = rust_min1(gexp(joint - joint0));
+#endif
     tna = 1;
 #pragma unroll
     for (int e = 0; e < E; ++e) { fq[e] = qe[e]; fp[e] = pe[e]; pr[e] = qe[e]; }
@@ -561,7 +573,11 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       long long ln_, lna;
       T lal;
       stack_scalars(k, lal, ln_, lna);
+#ifdef GM_AB_NOMIX  // A/B timing only (wrong results)
+      const double u = 0.5;
+#else
       const double u = nuts_u<double>(key, 64u + merge_ctr++);
+#endif
       const long long den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
       if (!(u < (double)tn / (double)den)) stack_vec(k, 2, pr);
       tn = ln_ + tn;
@@ -631,7 +647,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       eps_bar = gexp(((T)1 - eta) * glog(eps_bar) + eta * glog(eps));
       // RunningCov::update inside the collection window (:897-903, 108-129)
       const long long lim = a.n_discard > a.eb ? a.n_discard - a.eb : 0;
-      if (a.mass_mode && m > a.sb && m < lim) {
+      if (MASS && a.mass_mode && m > a.sb && m < lim) {
         rn += 1;
         const T ns = (T)rn;
         T d1[E], d2[E];
@@ -663,7 +679,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     starting = true;
   }
   if (track) tr.store(a.trk, c, lane, D);
-  if (a.mass_mode) {
+  if (MASS && a.mass_mode) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;

@@ -473,7 +473,10 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
         const long long threads = C * LPC;
         const unsigned blocks = (unsigned)((threads + 255) / 256);
         const size_t lds = size_lds(blocks, t.template lds_bytes<LPC, E>(), LPC, E, sizeof(T));
-        hipLaunchKernelGGL((nuts_kernel<T, LPC, E, TG>), dim3(blocks), dim3(256), lds, st, a, t);
+        if (a.mass_mode)
+          hipLaunchKernelGGL((nuts_kernel<T, LPC, E, TG, true>), dim3(blocks), dim3(256), lds, st, a, t);
+        else
+          hipLaunchKernelGGL((nuts_kernel<T, LPC, E, TG, false>), dim3(blocks), dim3(256), lds, st, a, t);
         return hipGetLastError();
       });
     }

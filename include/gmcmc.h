@@ -42,7 +42,10 @@ extern "C" {
 #define GM_ERCCL 4  /* RCCL error */
 #define GM_ESTATE 5 /* call not valid in the sampler's current state */
 
-typedef enum gm_dtype { GM_F32 = 0, GM_F64 = 1 } gm_dtype;
+/* GM_DTYPE_INT_: not a dtype; it widens the enum's value range to int, so a
+ * caller passing any other integer gets GM_EINVAL instead of undefined
+ * behaviour in the C++ implementation (found by the UBSan host build). */
+typedef enum gm_dtype { GM_F32 = 0, GM_F64 = 1, GM_DTYPE_INT_ = 0x7fffffff } gm_dtype;
 
 /* ---- targets (replaces the user-implemented traits) ---------------------
  * BatchedGradientTarget::unnorm_logp_batch   distributions.rs:67-78
@@ -388,6 +391,13 @@ int gm_bv_energy_ln(gm_dtype dtype, int64_t n, const void* a, void* out);
  * (NaN -> 0) */
 int gm_bv_accept_mask(gm_dtype dtype, int64_t n, const void* log_accept, const void* ln_u,
                       uint8_t* mask);
+/* EuclideanVector's remaining in-place ops on a [n] device vector
+ * (euclidean.rs:11-60): scale_assign x = x * alpha (:396-398); fill
+ * (fill_zero / zeros_like with value 0); dot = sum of a*b over all elements
+ * (:400-403) into a host double (T partials, fixed order). */
+int gm_bv_scale_assign(gm_dtype dtype, int64_t n, void* x, double alpha);
+int gm_bv_fill(gm_dtype dtype, int64_t n, void* x, double value);
+int gm_bv_dot(gm_dtype dtype, int64_t n, const void* a, const void* b, double* out);
 
 /* A built-in target resident on the device, for logp_and_grad on device
  * buffers (BatchedHamiltonianTarget, batched_hmc.rs:18-22; hmc.rs:42-61). */

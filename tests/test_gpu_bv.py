@@ -154,3 +154,25 @@ def test_writers_stream_device_samples(gm, tmp_path, monkeypatch):
     gio.save_parquet_tensor(ds, str(tmp_path / "dt.parquet"))
     gio.save_parquet_tensor(host.transpose(1, 0, 2), str(tmp_path / "ht.parquet"))
     assert pq.read_table(str(tmp_path / "dt.parquet")).equals(pq.read_table(str(tmp_path / "ht.parquet")))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_euclidean_scale_fill_dot(bv, dtype):
+    """EuclideanVector's remaining ops (euclidean.rs:11-56) the Rust seam of
+    INTEGRATION.md binds: scale_assign bitwise, fill, and dot against a float64
+    sum (summation order is the engine's: 1024 strided partials, then a tree)."""
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((129, 33)).astype(dtype)
+    y = rng.standard_normal((129, 33)).astype(dtype)
+    dx, dy = bv.DeviceMatrix.from_host(x), bv.DeviceMatrix.from_host(y)
+    a = dtype(0.37)
+    bv.scale_assign(dx, a)
+    np.testing.assert_array_equal(dx.to_host(), x * a)
+    got = bv.dot(dx, dy)
+    ref = float(np.sum((x * a).astype(np.float64) * y.astype(np.float64)))
+    assert abs(got - ref) <= (1e-4 if dtype == np.float32 else 1e-12) * max(1.0, abs(ref))
+    bv.fill(dy, 0.0)
+    assert not dy.to_host().any()
+    bv.fill(dy, 2.5)
+    assert (dy.to_host() == dtype(2.5)).all()
+    assert bv.dot(bv.DeviceMatrix((0,), dtype), bv.DeviceMatrix((0,), dtype)) == 0.0
