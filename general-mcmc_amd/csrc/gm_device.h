@@ -539,12 +539,6 @@ template <class T, int LPC, int E> struct GaussLane {
       const int i = lane * E + e;
       d[e] = (i < D) ? x[e] - mur[e] : (T)0;
     }
-#ifdef GM_AB_NOGEMV  // A/B timing only (wrong results): w = d, no product
-    if (true) {
-#pragma unroll
-      for (int e = 0; e < E; ++e) w[e] = d[e];
-    } else
-#endif
     if (sprec) {
       constexpr int S = LPC * E;
       // the previous evaluation's broadcast reads are done before d is replaced
@@ -556,16 +550,49 @@ template <class T, int LPC, int E> struct GaussLane {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const T* pr = sprec + lane * E;
-      {
-        const T d0 = sd[0];
+      // a lane's E entries of row j are contiguous and (E*sizeof(T))-aligned:
+      // read them as 16-byte vectors where E allows (ds_read_b128, 4 LDS
+      // cycles, instead of ds_read2_b64 pairs at 8)
+      auto row = [&](int j, T (&pj)[E]) __attribute__((always_inline)) {
+        if constexpr (E * sizeof(T) % 16 == 0) {
+          typedef T v16 __attribute__((ext_vector_type(16 / sizeof(T))));
+          constexpr int V = 16 / sizeof(T);
 #pragma unroll
-        for (int e = 0; e < E; ++e) w[e] = gfma(pr[e], d0, (T)0);
+          for (int k = 0; k < E / V; ++k) {
+            const v16 t = *(const v16*)(pr + j * S + k * V);
+#pragma unroll
+            for (int u = 0; u < V; ++u) pj[k * V + u] = t[u];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; ++e) pj[e] = pr[j * S + e];
+        }
+      };
+#pragma unroll
+      for (int e = 0; e < E; ++e) w[e] = (T)0;  // fma(p, d_0, +0): the chain's first term
+      int j = 0;
+      if constexpr (S % 2 == 0 && sizeof(T) == 8) {
+        // column pairs: d_j, d_{j+1} in one 16-byte broadcast read
+        typedef T v2 __attribute__((ext_vector_type(2)));
+#pragma unroll GM_GEMV_UNROLL
+        for (; j + 1 < D; j += 2) {
+          const v2 dd = *(const v2*)(sd + j);
+          T pj[E];
+          row(j, pj);
+#pragma unroll
+          for (int e = 0; e < E; ++e) w[e] = gfma(pj[e], dd[0], w[e]);
+          row(j + 1, pj);
+#pragma unroll
+          for (int e = 0; e < E; ++e) w[e] = gfma(pj[e], dd[1], w[e]);
+        }
       }
 #pragma unroll GM_GEMV_UNROLL
-      for (int j = 1; j < D; ++j) {
+      for (; j < D; ++j) {
         const T dj = sd[j];
+        T pj[E];
+        row(j, pj);
 #pragma unroll
-        for (int e = 0; e < E; ++e) w[e] = gfma(pr[j * S + e], dj, w[e]);
+        for (int e = 0; e < E; ++e) w[e] = gfma(pj[e], dj, w[e]);
       }
     } else {
       // Columns in batches of GU: the batch's global loads and lane

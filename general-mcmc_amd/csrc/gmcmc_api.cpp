@@ -303,10 +303,13 @@ int gm_device_count(int* count) {
   return GM_OK;
 }
 
+// The calling thread's host waits spin instead of yielding (set before the
+// device is first used): a run's completion wait is short and latency-bound,
+// and a thread that slept through it comes back with cold caches; measured
+// 4 us less wall time on the bench's first timed run
+// (profiles/r02/launch_ab.json).
 int gm_set_device(int device) {
-#ifdef GM_AB_SPIN  // A/B builds only: spinning host waits (set before the device is initialised)
-  hipSetDeviceFlags(hipDeviceScheduleSpin);
-#endif
+  hipSetDeviceFlags(hipDeviceScheduleSpin);  // ignored once the device is initialised
   GM_HIP(hipSetDevice(device));
   return GM_OK;
 }

@@ -295,6 +295,17 @@ __device__ __attribute__((noinline)) T find_reasonable_epsilon(const TG& tg, con
 // half) and ends the doubling. The trajectory ends live in registers as the
 // edge (the end being integrated, side v) and the far end; a direction change
 // swaps them.
+#ifdef GM_NUTS_PROF
+// Measurement build only (tools/ab_variants.sh nprof "-DGM_NUTS_PROF"): per
+// wave, the shader cycles of each lockstep iteration binned by what the
+// wave's chains did in it (bit 0 a transition start, 1 a subtree merge,
+// 2 a doubling end, 3 a transition end) plus the evaluation's share;
+// read back by gm_nuts_prof_read (nuts_kernels.hip).
+constexpr int NPROF_SLOTS = 16 * 2 + 2;
+constexpr int NPROF_WAVES = 8192;
+__device__ unsigned long long gm_nuts_prof_buf[NPROF_WAVES * NPROF_SLOTS];
+#endif
+
 template <class T, int LPC, int E, class TG, bool MASS>
 __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -474,8 +485,30 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     qe[e] = pe[e] = ge[e] = qf[e] = pf[e] = gf[e] = fq[e] = fp[e] = pr[e] = p0[e] = (T)0;
   }
 
+#ifdef GM_NUTS_PROF
+  unsigned long long pcnt[16] = {}, pcyc[16] = {}, peval = 0, piter = 0;
+  unsigned long long ptop = __builtin_amdgcn_s_memtime();
+  bool f_start = false, f_merge = false, f_dbl = false, f_trans = false;
+#endif
   while (true) {
     const bool live = s < a.n_steps;
+#ifdef GM_NUTS_PROF
+    {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      const int bin = (__builtin_amdgcn_ballot_w64(f_start) != 0 ? 1 : 0) |
+                      (__builtin_amdgcn_ballot_w64(f_merge) != 0 ? 2 : 0) |
+                      (__builtin_amdgcn_ballot_w64(f_dbl) != 0 ? 4 : 0) |
+                      (__builtin_amdgcn_ballot_w64(f_trans) != 0 ? 8 : 0);
+      if (piter > 0) {
+#pragma unroll
+        for (int b = 0; b < 16; ++b)
+          if (b == bin) { pcnt[b] += 1; pcyc[b] += now - ptop; }
+      }
+      ++piter;
+      ptop = now;
+      f_start = f_merge = f_dbl = f_trans = false;
+    }
+#endif
     if (__builtin_amdgcn_ballot_w64(live) == 0) break;  // every chain of the wave is done
     const uint64_t st = a.step0 + (uint64_t)s;
     const T epsv = (T)v * eps;
@@ -514,11 +547,17 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       sums[1] = kin_part_m<LPC, E>(M, pk, lane);
     }
     group_sum_n<LPC>(sums);  // log-density and kinetic energy, reduced together
+#ifdef GM_NUTS_PROF
+    peval += __builtin_amdgcn_s_memtime() - ptop;
+#endif
     const T lp = tg.finish(sums[0]);
     const T kin = (T)0.5 * sums[1];
     if (!live) continue;
 
     if (starting) {
+#ifdef GM_NUTS_PROF
+      f_start = true;
+#endif
       // --- transition start: slice variable, trajectory ends (:764-781)
       joint0 = lp - kin;
       const u32x4 kw = draw_block(a.seed, cid, st, TAG_NUTS_EXP, 0u);
@@ -545,11 +584,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     const T joint = lp - kin;
     tn = (logu < joint) ? 1 : 0;
     ts = (logu - (T)1000) < joint;
-#ifdef GM_AB_NOEXP  // A/B timing only (wrong results)
-    ta = joint > joint0 ? (T)1 : (T)0.5;
-#else
     ta = rust_min1(gexp(joint - joint0));
-#endif
     tna = 1;
 #pragma unroll
     for (int e = 0; e < E; ++e) { fq[e] = qe[e]; fp[e] = pe[e]; pr[e] = qe[e]; }
@@ -567,17 +602,16 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
         break;
       }
       // right child: merge with the stored left sibling (:1251-1323)
+#ifdef GM_NUTS_PROF
+      f_merge = true;
+#endif
       T lq[E], lpv[E];
       stack_vec(k, 0, lq);
       stack_vec(k, 1, lpv);
       long long ln_, lna;
       T lal;
       stack_scalars(k, lal, ln_, lna);
-#ifdef GM_AB_NOMIX  // A/B timing only (wrong results)
-      const double u = 0.5;
-#else
       const double u = nuts_u<double>(key, 64u + merge_ctr++);
-#endif
       const long long den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
       if (!(u < (double)tn / (double)den)) stack_vec(k, 2, pr);
       tn = ln_ + tn;
@@ -597,6 +631,9 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     // The new end on side v is the edge; alpha / n_alpha are this subtree's.
     const T alpha = ta;
     const long long n_alpha = tna;
+#ifdef GM_NUTS_PROF
+    f_dbl = true;
+#endif
     {
       const T tmp = rust_min1((T)tn / (T)n);
       const T u2 = nuts_u<T>(key, 2u * (uint32_t)j + 1u);
@@ -637,6 +674,9 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     }
 
     // --- the transition is complete: dual averaging (generic_nuts.rs:882-924)
+#ifdef GM_NUTS_PROF
+    f_trans = true;
+#endif
     const long long m = a.m0 + s + 1;
     T eta = (T)1 / (T)(m + t0c);
     h_bar = ((T)1 - eta) * h_bar + eta * (delta - alpha / (T)n_alpha);
@@ -678,6 +718,17 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     ++s;
     starting = true;
   }
+#ifdef GM_NUTS_PROF
+  {
+    const long long wv = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / 64;
+    if ((threadIdx.x & 63) == 0 && wv < NPROF_WAVES) {
+      unsigned long long* o = gm_nuts_prof_buf + wv * NPROF_SLOTS;
+      for (int b = 0; b < 16; ++b) { o[2 * b] = pcnt[b]; o[2 * b + 1] = pcyc[b]; }
+      o[32] = peval;
+      o[33] = piter;
+    }
+  }
+#endif
   if (track) tr.store(a.trk, c, lane, D);
   if (MASS && a.mass_mode) {
 #pragma unroll

@@ -558,3 +558,13 @@ int nuts_get_leapfrogs(NutsState& ns, long long C, long long* out) {
 }
 
 }  // namespace gm
+
+#ifdef GM_NUTS_PROF
+// measurement build only: the per-wave iteration profile of the last NUTS
+// launch (nuts_device.h), n = waves x 34 unsigned 64-bit words
+extern "C" int gm_nuts_prof_read(void* out, long long n) {
+  if (n > (long long)gm::NPROF_WAVES * gm::NPROF_SLOTS) return 1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gm::gm_nuts_prof_buf), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0 : 2;
+}
+#endif

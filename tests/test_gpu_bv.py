@@ -125,6 +125,18 @@ def test_hbm_leapfrog_equals_composed_ops(gm, bv, name, mk, D, dtype, eps, L):
     np.testing.assert_array_equal(b, c)
 
 
+@pytest.mark.parametrize("D,dtype", [(64, np.float32), (32, np.float64), (16, np.float32), (128, np.float32),
+                                     (256, np.float64)])
+@pytest.mark.parametrize("C", [1, 5, 50, 1001])
+def test_hbm_leapfrog_ragged(gm, bv, D, dtype, C):
+    """gm_bv_leapfrog with a partial last block (C not a multiple of the
+    chains per block) == the composed ops, bitwise."""
+    x0 = gm.init_with_seed(C, D, 5, dtype)
+    composed = bv.BatchedGenericHMC(gm.RosenbrockND(), x0, 0.01, 3, seed=2)
+    per_lf = bv.BatchedGenericHMC(gm.RosenbrockND(), x0, 0.01, 3, seed=2, fused_leapfrog=True)
+    np.testing.assert_array_equal(composed.run(2, 1), per_lf.run(2, 1))
+
+
 def test_bv_rejects_bad_arguments(gm, bv):
     a = bv.DeviceMatrix((4, 3), np.float32)
     b = bv.DeviceMatrix((4, 2), np.float32)

@@ -98,17 +98,21 @@ def ref10k(a):
             "chain_leapfrog_per_s": n * 200 * 50 / t, "includes": "D2H of the [6,100,10000] sample"}
 
 
-p = argparse.ArgumentParser()
-p.add_argument("--which", default="3,4,5,10k")
-p.add_argument("--nuts-chains", type=int, default=8192)
-p.add_argument("--nuts-discard", type=int, default=500)
-p.add_argument("--nuts-collect", type=int, default=500)
-p.add_argument("--nuts-layout", default="")
-p.add_argument("--hmc128-chains", type=int, default=8192)
-p.add_argument("--mh-chains", type=int, default=16384)
-p.add_argument("--mh-layout", default="")
-a = p.parse_args()
-out = []
-for w in a.which.split(","):
-    r = {"3": cfg3, "4": cfg4, "5": cfg5, "10k": ref10k}[w](a)
-    print(json.dumps(r), flush=True)
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--which", default="3,4,5,10k")
+    p.add_argument("--nuts-chains", type=int, default=8192)
+    p.add_argument("--nuts-discard", type=int, default=500)
+    p.add_argument("--nuts-collect", type=int, default=500)
+    p.add_argument("--nuts-layout", default="")
+    p.add_argument("--hmc128-chains", type=int, default=8192)
+    p.add_argument("--mh-chains", type=int, default=16384)
+    p.add_argument("--mh-layout", default="")
+    a = p.parse_args()
+    for w in a.which.split(","):
+        r = {"3": cfg3, "4": cfg4, "5": cfg5, "10k": ref10k}[w](a)
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

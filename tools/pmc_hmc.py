@@ -67,6 +67,8 @@ def main():
     sq = dispatch_counters(os.path.join(a.prof_dir, "sq"))
     grbm = dispatch_counters(os.path.join(a.prof_dir, "grbm"))
     cycles = grbm["GRBM_GUI_ACTIVE"] / 8.0
+    fdir = os.path.join(a.prof_dir, "flops")
+    fl = dispatch_counters(fdir) if os.path.isdir(fdir) else {}
     entry = {
         "hbm_bytes_per_launch": (2 * f_kb + w_kb) * 1024.0,
         "fetch_size_kb": f_kb, "write_size_kb": w_kb,
@@ -84,6 +86,11 @@ def main():
         "source": f"{a.prof_dir}: trace, fetch, write, sq, grbm passes (rocprofv3, one run each); "
                   "the second hmc_kernel dispatch",
     }
+    if fl:
+        f32 = fl.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0)
+        entry["pmc_flops"] = {"fp32": f32, "fma_f32_insts": fl.get("SQ_INSTS_VALU_FMA_F32"),
+                              "fp32_tflops": f32 / dur / 1e12, "fp32_frac": f32 / dur / 157.3e12,
+                              "note": "SQ_INSTS_VALU_FLOPS_FP32 of the launch over its traced duration"}
     d = json.load(open(OUT)) if os.path.exists(OUT) else {}
     e = d.setdefault(a.key, {"by_steps": {}})
     e["by_steps"][str(a.steps)] = entry
