@@ -25,6 +25,7 @@
 #include "nuts_device.h"
 #include "gm_jit.h"
 #include "gm_layouts.h"
+#include "nuts_launch.h"
 #include "gm_nuts.h"
 #include "gm_track.h"
 
@@ -380,16 +381,17 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
   }
   int pending_refind = 0;
   uint64_t refind_step = 0;
-  const long long lds_cap = ns.lds_levels_cap;  // gm_nuts_set_lds_levels (-1: as many as fit)
-  int ncu = 256, lds_max = 64 * 1024;
+  NutsLdsBudget budget;
+  budget.lds_cap = ns.lds_levels_cap;  // gm_nuts_set_lds_levels (-1: as many as fit)
   {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1)
-      ncu = 256;
-    if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess ||
-        lds_max < 1)
-      lds_max = 64 * 1024;
+        hipDeviceGetAttribute(&budget.ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        budget.ncu < 1)
+      budget.ncu = 256;
+    if (hipDeviceGetAttribute(&budget.lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess ||
+        budget.lds_max < 1)
+      budget.lds_max = 64 * 1024;
   }
   for (long long li = 0; li < n_launch; ++li) {
     const long long start = seg_start[li], nst = seg_len[li];
@@ -443,42 +445,15 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
       a.trk.n0 = trk->n0 + (unsigned long long)start;
     }
     hipEventRecord(evs[2 * li], st);
-    // LDS: the target's staging area (tgl bytes), then as many subtree-stack
-    // levels as fit in the CU's 160 KiB shared by the grid's blocks per CU
-    // (at most 4: the kernel's VGPRs allow no more); returns the dynamic LDS
-    // size and sets a.lds_*
-    auto size_lds = [&](unsigned blocks, size_t tgl, int LPC, int E, size_t tsz) -> size_t {
-      tgl = (tgl + 15) / 16 * 16;
-      const size_t per_level = (size_t)3 * 256 * E * tsz + (size_t)(256 / LPC) * (tsz + 8);
-      long long bpc = ((long long)blocks + ncu - 1) / ncu;
-      bpc = bpc < 1 ? 1 : bpc > 4 ? 4 : bpc;
-      size_t budget = (size_t)(160 * 1024) / (size_t)bpc - 1024;
-      if (budget > (size_t)lds_max) budget = (size_t)lds_max;
-      long long kl = budget > tgl ? (long long)((budget - tgl) / per_level) : 0;
-      if (kl > a.max_depth) kl = a.max_depth;
-      if (lds_cap >= 0 && kl > lds_cap) kl = lds_cap;
-      a.lds_levels = (int)kl;
-      a.lds_stack_off = (unsigned)tgl;
-      return tgl + (size_t)kl * per_level;
-    };
     hipError_t e;
     if (tg.kind == GM_TARGET_CUSTOM) {  // user target, runtime-compiled (gm_jit.cpp)
       const unsigned blocks = (unsigned)((C + 255) / 256);
-      const size_t lds = size_lds(blocks, 0, 1, D, esz);
+      const size_t lds = nuts_size_lds(a, budget, blocks, 0, 1, D, esz);
       UserTargetArg ut{tg.params, tg.D};
       void* args[] = {&a, &ut};
       e = jit_launch(JIT_NUTS, dt, tg, blocks, 256, lds, st, args);
     } else {
-      e = dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
-        const long long threads = C * LPC;
-        const unsigned blocks = (unsigned)((threads + 255) / 256);
-        const size_t lds = size_lds(blocks, t.template lds_bytes<LPC, E>(), LPC, E, sizeof(T));
-        if (a.mass_mode)
-          hipLaunchKernelGGL((nuts_kernel<T, LPC, E, TG, true>), dim3(blocks), dim3(256), lds, st, a, t);
-        else
-          hipLaunchKernelGGL((nuts_kernel<T, LPC, E, TG, false>), dim3(blocks), dim3(256), lds, st, a, t);
-        return hipGetLastError();
-      });
+      e = nuts_launch_layout(dt, tg, lay, a, st, budget);
     }
     if (e != hipSuccess) {
       set_error(std::string("NUTS launch failed: ") + hipGetErrorString(e));
@@ -559,12 +534,3 @@ int nuts_get_leapfrogs(NutsState& ns, long long C, long long* out) {
 
 }  // namespace gm
 
-#ifdef GM_NUTS_PROF
-// measurement build only: the per-wave iteration profile of the last NUTS
-// launch (nuts_device.h), n = waves x 34 unsigned 64-bit words
-extern "C" int gm_nuts_prof_read(void* out, long long n) {
-  if (n > (long long)gm::NPROF_WAVES * gm::NPROF_SLOTS) return 1;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gm::gm_nuts_prof_buf), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess
-             ? 0 : 2;
-}
-#endif

@@ -1,0 +1,71 @@
+// nuts_launch.h — launch of the NUTS transition kernel for one compiled
+// layout. The (dtype, target, layout) instantiations are spread over the
+// translation units nuts_part0.hip ... nuts_part5.hip (three layouts each) so
+// that they compile in parallel; nuts_run (nuts_kernels.hip) asks each part in
+// turn.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "gm_internal.h"
+#include "gm_launch.h"
+
+namespace gm {
+
+// What the LDS sizing of a launch needs to know about the device and the
+// sampler (gm_nuts_set_lds_levels).
+struct NutsLdsBudget {
+  int ncu = 256;                // compute units
+  int lds_max = 64 * 1024;      // dynamic LDS per block
+  long long lds_cap = -1;       // levels cap (-1: as many as fit)
+};
+
+// LDS of a launch: the target's staging area (tgl bytes), then as many
+// subtree-stack levels as fit in the CU's 160 KiB shared by the grid's blocks
+// per CU (at most 4 blocks counted) and max_depth; sets a.lds_levels and
+// a.lds_stack_off, returns the dynamic LDS size.
+inline size_t nuts_size_lds(NutsLaunch& a, const NutsLdsBudget& b, unsigned blocks, size_t tgl, int LPC, int E,
+                            size_t tsz) {
+  tgl = (tgl + 15) / 16 * 16;
+  const size_t per_level = (size_t)3 * 256 * E * tsz + (size_t)(256 / LPC) * (tsz + 8);
+  long long bpc = ((long long)blocks + b.ncu - 1) / b.ncu;
+  bpc = bpc < 1 ? 1 : bpc > 4 ? 4 : bpc;
+  size_t budget = (size_t)(160 * 1024) / (size_t)bpc - 1024;
+  if (budget > (size_t)b.lds_max) budget = (size_t)b.lds_max;
+  long long kl = budget > tgl ? (long long)((budget - tgl) / per_level) : 0;
+  if (kl > a.max_depth) kl = a.max_depth;
+  if (b.lds_cap >= 0 && kl > b.lds_cap) kl = b.lds_cap;
+  a.lds_levels = (int)kl;
+  a.lds_stack_off = (unsigned)tgl;
+  return tgl + (size_t)kl * per_level;
+}
+
+// Launches nuts_kernel for (dt, tg, lay) when part `part` holds that layout
+// (*found = true), else returns hipSuccess with *found = false.
+hipError_t nuts_launch_part0(gm_dtype dt, const TargetDev& tg, const Layout& lay, NutsLaunch& a, hipStream_t st,
+                             const NutsLdsBudget& b, bool* found);
+hipError_t nuts_launch_part1(gm_dtype dt, const TargetDev& tg, const Layout& lay, NutsLaunch& a, hipStream_t st,
+                             const NutsLdsBudget& b, bool* found);
+hipError_t nuts_launch_part2(gm_dtype dt, const TargetDev& tg, const Layout& lay, NutsLaunch& a, hipStream_t st,
+                             const NutsLdsBudget& b, bool* found);
+hipError_t nuts_launch_part3(gm_dtype dt, const TargetDev& tg, const Layout& lay, NutsLaunch& a, hipStream_t st,
+                             const NutsLdsBudget& b, bool* found);
+hipError_t nuts_launch_part4(gm_dtype dt, const TargetDev& tg, const Layout& lay, NutsLaunch& a, hipStream_t st,
+                             const NutsLdsBudget& b, bool* found);
+hipError_t nuts_launch_part5(gm_dtype dt, const TargetDev& tg, const Layout& lay, NutsLaunch& a, hipStream_t st,
+                             const NutsLdsBudget& b, bool* found);
+
+inline hipError_t nuts_launch_layout(gm_dtype dt, const TargetDev& tg, const Layout& lay, NutsLaunch& a,
+                                     hipStream_t st, const NutsLdsBudget& b) {
+  using Fn = hipError_t (*)(gm_dtype, const TargetDev&, const Layout&, NutsLaunch&, hipStream_t,
+                            const NutsLdsBudget&, bool*);
+  static const Fn parts[] = {nuts_launch_part0, nuts_launch_part1, nuts_launch_part2,
+                             nuts_launch_part3, nuts_launch_part4, nuts_launch_part5};
+  for (Fn f : parts) {
+    bool found = false;
+    const hipError_t e = f(dt, tg, lay, a, st, b, &found);
+    if (found) return e;
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace gm

@@ -1,6 +1,6 @@
 #!/bin/bash
-# One GPU session: tests, smoke, bench. Each GPU step has its own time limit;
-# a crash/abort/timeout (status >= 124 or signal) ends the script.
+# One GPU session: probes, tests, smoke, bench. Each GPU step has its own time
+# limit; a crash/abort/timeout (status >= 124 or signal) ends the script.
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
 run() {  # name, seconds, command...
@@ -13,3 +13,19 @@ run() {  # name, seconds, command...
   if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then echo "fatal step $name ($rc), stopping" >&2; exit $rc; fi
   return $rc
 }
+for step in "$@"; do
+  case $step in
+    mfma) run mfma_probe 60 ./tools/probes/bin/gemv_mfma_probe 8192 200 ;;
+    tests) run gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench20) run bench20 300 python bench.py --steps 20 --warmup 5 ;;
+    bench) run bench 300 python bench.py ;;
+    configs) run configs 300 python tools/bench_configs.py ;;
+    mfma64) run mfma_f64_probe 60 ./tools/probes/bin/mfma_f64_probe ;;
+    first)
+      for v in "" "--extra-warm 1" "--sleep-ms 5" "--warm-collect" "" "--extra-warm 1" "--sleep-ms 5" "--warm-collect"; do
+        run first_call 60 python tools/probe_bench_first.py --repeat 4 $v && cat gpurun_out/first_call.log >> gpurun_out/first_calls.jsonl
+      done ;;
+    nprof) run nuts_prof 120 env GMCMC_LIB=abtest/nprof/libgmcmc.so python tools/probe_nuts_prof.py ;;
+  esac
+done
