@@ -462,6 +462,24 @@ template <class T> struct IsoGaussT {
 // no lane needs a bounds test), and each evaluation publishes d in a per-group
 // LDS slot from which coordinate j is read as a broadcast: per column one LDS
 // read of P and one broadcast read of d_j, no shuffles, no global loads.
+//
+// Matrix-core form (f64, 16 lanes x 2 coordinates per chain, D <= 32: NUTS
+// cfg3's layout). A wave holds 4 chains; w = P [d_0 .. d_3] is a 32x32 by
+// 32x4 product, 16 v_mfma_f64_4x4x4_4b_f64 (two 16-row halves g x eight
+// 4-column steps s; the 4 blocks of an instruction are the 4 row tiles of a
+// half, the 4 columns of a block are the wave's 4 chains). Measured on gfx950
+// (tools/probes/mfma_f64_probe.hip, profiles/r02/mfma/): the instruction's
+// result is bit for bit the k-ascending fma chain from C, so accumulating s
+// ascending from C = +0 is exactly the oracle's j-ascending chain; lane
+// l = 16r + 4b + q holds A[m=q][k=r], B[k=r][n=q] and C/D[m=r][n=q] of block
+// b. bind() stages P once per block in fragment order (lane l's 16 A values
+// as 8 16-byte pairs); an evaluation publishes d transposed (slot [r][s] =
+// d_{4s+r}, so a lane's 8 B values are 64 contiguous bytes), issues the 16
+// instructions, and routes w back to the chains' lanes through a second
+// slot. All 64 lanes take part, so the form runs only with the whole wave
+// active (a partial last wave, or a chain-divergent call such as the step
+// size search, takes the global-memory VALU product: the same chain, so the
+// same bits).
 extern __shared__ __attribute__((aligned(16))) unsigned char gm_dyn_lds[];
 
 // fused multiply-add, one rounding (the oracle's FMA)
@@ -476,8 +494,13 @@ template <class T> struct GaussT {
   T nc;
   int D;
   int use_lds = 0;
+  // the matrix-core form applies to layout (LPC, E) (at D <= 32)
+  template <int LPC, int E> __host__ __device__ static constexpr bool mfma_form() {
+    return sizeof(T) == 8 && LPC == 16 && E == 2;
+  }
   // dynamic LDS bytes a 256-thread block needs for layout (LPC, E)
   template <int LPC, int E> __host__ __device__ static size_t lds_need(int D) {
+    if (mfma_form<LPC, E>() && D <= 32) return ((size_t)1024 + (size_t)2 * 256 * E) * sizeof(T);
     return ((size_t)D * LPC * E + (size_t)256 * E) * sizeof(T);
   }
   template <int LPC, int E> __host__ __device__ size_t lds_bytes() const {
@@ -493,6 +516,22 @@ template <class T> struct GaussT {
     r.D = D;
     r.sprec = nullptr;
     r.sd = nullptr;
+    r.mf = false;
+    if constexpr (mfma_form<LPC, E>()) {
+      if (use_lds && D <= 32) {  // fragment order: k = (pair * 64 + lane) * 2 + (f & 1), f = 8g + s
+        T* sp = (T*)gm_dyn_lds;
+        for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
+          const int l = (k >> 1) & 63, f = ((k >> 7) << 1) | (k & 1);
+          const int row = 16 * (f >> 3) + 4 * ((l >> 2) & 3) + (l & 3), col = 4 * (f & 7) + (l >> 4);
+          sp[k] = (row < D && col < D) ? prec[(long long)col * D + row] : (T)0;
+        }
+        __syncthreads();
+        r.sprec = sp;
+        r.sd = sp + 1024 + (threadIdx.x >> 4) * 32;
+        r.mf = true;
+        return r;
+      }
+    }
     if (use_lds) {  // every thread of the block reaches bind() (kernels return after it)
       constexpr int S = LPC * E;
       T* sp = (T*)gm_dyn_lds;
@@ -514,8 +553,9 @@ template <class T, int LPC, int E> struct GaussLane {
   const T* prec;
   T nc;
   int D;
-  const T* sprec;  // LDS [D][S] or null
-  T* sd;           // LDS slot of this lane group's d [S]
+  const T* sprec;  // LDS [D][S], or the matrix-core fragments (mf), or null
+  T* sd;           // LDS slot of this lane group's d [S] (mf: transposed [4][8])
+  bool mf;         // matrix-core form (see above)
   // unreduced log-density term for callers that reduce it together with
   // another per-chain sum: logp = finish(group_sum(eval_part(...)))
   template <int LPC_> static constexpr bool has_part = true;
@@ -530,6 +570,50 @@ template <class T, int LPC, int E> struct GaussLane {
     if (LOGP) return finish(group_sum<LPC>(part));
     return (T)0;
   }
+  // w = P d of the wave's 4 chains on the matrix cores (the form above)
+  __device__ __forceinline__ void mfma_product(const T (&d)[E], T (&w)[E]) const {
+    if constexpr (GaussT<T>::template mfma_form<LPC, E>()) {
+      typedef double v2 __attribute__((ext_vector_type(2)));
+      const int l = threadIdx.x & 63;
+      const int wb = (threadIdx.x >> 6) * 4;  // the wave's first chain slot in the block
+      // the previous evaluation's reads of the slots are done before they are replaced
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int j = (l & 15) * E + e;
+        sd[(j & 3) * 8 + (j >> 2)] = d[e];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // B: chain l&3's d_{4s + (l>>4)}, s = 0..7
+      const T* bt = sprec + 1024 + (wb + (l & 3)) * 32 + (l >> 4) * 8;
+      v2 bv[4], av[8];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bv[t] = *(const v2*)(bt + 2 * t);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) av[t] = *(const v2*)(sprec + (t * 64 + l) * 2);
+      double acc0 = 0.0, acc1 = 0.0;  // rows 4b + (l>>4) of the halves g = 0, 1
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        const double b = bv[s >> 1][s & 1];
+        acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(av[s >> 1][s & 1], b, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(av[4 + (s >> 1)][s & 1], b, acc1, 0, 0, 0);
+      }
+      // D[m = l>>4][n = l&3] of block (l>>2)&3: chain l&3's w at row 4((l>>2)&3) + (l>>4) (+16)
+      T* ws = const_cast<T*>(sprec) + 1536;
+      const int row = 4 * ((l >> 2) & 3) + (l >> 4);
+      ws[(wb + (l & 3)) * 32 + row] = acc0;
+      ws[(wb + (l & 3)) * 32 + 16 + row] = acc1;
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const v2 wv = *(const v2*)(ws + (threadIdx.x >> 4) * 32 + (l & 15) * E);
+      w[0] = wv[0];
+      w[1] = wv[1];
+    }
+  }
   template <int LPC_, int E_, bool LOGP>
   __device__ __forceinline__ T eval_impl(const T (&x)[E], T (&g)[E], int lane) const {
     static_assert(LPC_ == LPC && E_ == E, "layout mismatch");
@@ -539,7 +623,15 @@ template <class T, int LPC, int E> struct GaussLane {
       const int i = lane * E + e;
       d[e] = (i < D) ? x[e] - mur[e] : (T)0;
     }
-    if (sprec) {
+    bool done = false;
+    if constexpr (GaussT<T>::template mfma_form<LPC, E>()) {
+      if (mf && __builtin_amdgcn_read_exec() == ~0ull) {
+        mfma_product(d, w);
+        done = true;
+      }
+    }
+    if (done) {
+    } else if (sprec && !mf) {
       constexpr int S = LPC * E;
       // the previous evaluation's broadcast reads are done before d is replaced
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -17,13 +17,14 @@ for step in "$@"; do
   case $step in
     mfma) run mfma_probe 60 ./tools/probes/bin/gemv_mfma_probe 8192 200 ;;
     tests) run gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    mfmatest) run mfma_tests 300 python -u -m pytest tests/test_gpu_mfma_gauss.py -x -q --timeout 120 --timeout-method thread ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) run bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench) run bench 300 python bench.py ;;
     configs) run configs 300 python tools/bench_configs.py ;;
     mfma64) run mfma_f64_probe 60 ./tools/probes/bin/mfma_f64_probe ;;
     first)
-      for v in "" "--extra-warm 1" "--sleep-ms 5" "--warm-collect" "" "--extra-warm 1" "--sleep-ms 5" "--warm-collect"; do
+      for v in "--warm-collect" "--warm-collect --scratch-warm 1" "--warm-collect --scratch-warm 2" "--warm-collect" "--warm-collect --scratch-warm 1" "--warm-collect --scratch-warm 2"; do
         run first_call 60 python tools/probe_bench_first.py --repeat 4 $v && cat gpurun_out/first_call.log >> gpurun_out/first_calls.jsonl
       done ;;
     nprof) run nuts_prof 120 env GMCMC_LIB=abtest/nprof/libgmcmc.so python tools/probe_nuts_prof.py ;;

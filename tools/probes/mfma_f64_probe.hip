@@ -25,7 +25,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 __global__ void k4(const double* a, const double* b, const double* c, double* d, int T) {
   const int l = threadIdx.x;
   for (int t = 0; t < T; ++t)
-    d[t * 64 + l] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[t * 64 + l], b[t * 64 + l], c[t * 64 + l], 0, 0, 0);
+    d[t * 64 + l] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[t * 64 + l], b[t * 64 + l], c[t * 256 + l], 0, 0, 0);
 }
 __global__ void k16(const double* a, const double* b, const double* c, double* d, int T) {
   const int l = threadIdx.x;
@@ -34,6 +34,17 @@ __global__ void k16(const double* a, const double* b, const double* c, double* d
     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[t * 64 + l], b[t * 64 + l], acc, 0, 0, 0);
     for (int r = 0; r < 4; ++r) d[t * 256 + l * 4 + r] = acc[r];
   }
+}
+
+// one-hot decode of the 4x4x4_4b maps: A = e_la, B[l] = l + 1, C = 0
+__global__ void k4hot(double* d) {
+  const int l = threadIdx.x;
+  for (int la = 0; la < 64; ++la)
+    d[la * 64 + l] = __builtin_amdgcn_mfma_f64_4x4x4f64(l == la ? 1.0 : 0.0, (double)(l + 1), 0.0, 0, 0, 0);
+}
+__global__ void k4hotc(double* d) {  // C one-hot, A = B = 0: where C[l] lands in D
+  const int l = threadIdx.x;
+  for (int lc = 0; lc < 64; ++lc) d[lc * 64 + l] = __builtin_amdgcn_mfma_f64_4x4x4f64(0.0, 0.0, l == lc ? 1.0 : 0.0, 0, 0, 0);
 }
 
 // timing: R rounds of N dependent (chains = 1) or 4 independent chains
@@ -94,7 +105,28 @@ static double dot4(const double* a, const double* b, double c, Mode m) {
 
 // 4x4x4_4b candidate maps: within block b = l/16, i = l%16; sel bit 0: A[m=i%4][k=i/4] (0) or A[m=i/4][k=i%4] (1);
 // bit 1: B[k=i/4][n=i%4] (0) or B[k=i%4][n=i/4] (1); bit 2: D[m=i/4][n=i%4] (0) or D[m=i%4][n=i/4] (1)
+// sel 8: the map decoded from the one-hot runs below: lane l = 16r + 4*blk + q holds A[m=q][k=r],
+// B[k=r][n=q], C/D[m=r][n=q] of block blk
 static void model4(const double* a, const double* b, const double* c, double* d, int sel, Mode mode) {
+  if (sel == 8) {
+    for (int blk = 0; blk < 4; ++blk) {
+      double A[4][4], B[4][4], Cm[4][4];
+      for (int r = 0; r < 4; ++r)
+        for (int q = 0; q < 4; ++q) {
+          const int l = 16 * r + 4 * blk + q;
+          A[q][r] = a[l];
+          B[r][q] = b[l];
+          Cm[r][q] = c[l];
+        }
+      for (int r = 0; r < 4; ++r)
+        for (int q = 0; q < 4; ++q) {
+          double ar[4], br[4];
+          for (int k = 0; k < 4; ++k) { ar[k] = A[r][k]; br[k] = B[k][q]; }
+          d[16 * r + 4 * blk + q] = dot4(ar, br, Cm[r][q], mode);
+        }
+    }
+    return;
+  }
   for (int blk = 0; blk < 4; ++blk) {
     double A[4][4], B[4][4], Cm[4][4];
     for (int i = 0; i < 16; ++i) {
@@ -167,7 +199,7 @@ int main() {
     CK(hipMemcpy(d16.data(), dd, 8 * d16.size(), hipMemcpyDeviceToHost));
     const char* mname[3] = {"fma_k_ascending", "fma_k_descending", "rounded_products_summed"};
     printf("%s\"%s\": {\"mfma_4x4x4_4b\": {", phase ? ", " : "", phase ? "rounding_spread_doubles" : "maps_small_integers");
-    for (int sel = 0; sel < 8; ++sel)
+    for (int sel = 0; sel < 9; ++sel)
       for (int mo = 0; mo < 3; ++mo) {
         if (phase == 0 && mo > 0) continue;
         long long bad = 0;
@@ -193,17 +225,46 @@ int main() {
       }
     printf("}, \"outputs_per_form\": [%d, %d]}", T * 64, T * 256);
   }
+  {
+    std::vector<double> h(64 * 64);
+    hipLaunchKernelGGL(k4hot, dim3(1), dim3(64), 0, 0, dd);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(h.data(), dd, 8 * h.size(), hipMemcpyDeviceToHost));
+    printf(", \"onehot_A_4x4x4\": [");
+    for (int la = 0; la < 64; ++la) {
+      printf("%s\"%d:", la ? ", " : "", la);
+      for (int l = 0; l < 64; ++l)
+        if (h[la * 64 + l] != 0) printf(" %d<-B%d", l, (int)h[la * 64 + l] - 1);
+      printf("\"");
+    }
+    printf("]");
+    hipLaunchKernelGGL(k4hotc, dim3(1), dim3(64), 0, 0, dd);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(h.data(), dd, 8 * h.size(), hipMemcpyDeviceToHost));
+    printf(", \"onehot_C_4x4x4\": \"");
+    for (int lc = 0; lc < 64; ++lc)
+      for (int l = 0; l < 64; ++l)
+        if (h[lc * 64 + l] != 0) printf(" C%d->D%d", lc, l);
+    printf("\"");
+  }
   // timing, one wave per SIMD (1024 waves of 64 on 256 CUs x 4 SIMDs) and one wave alone
   double* dout;
   long long* dcyc;
-  CK(hipMalloc(&dout, 8 * 1024 * 64));
-  CK(hipMalloc(&dcyc, 8 * 1024));
+  CK(hipMalloc(&dout, 8 * 2048 * 64));
+  CK(hipMalloc(&dcyc, 8 * 2048));
   const int R = 4096;
-  auto run = [&](void (*k)(double*, int, long long*), int blocks, int per) {
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(64), 0, 0, dout, R, dcyc);
-    CK(hipDeviceSynchronize());
-    hipLaunchKernelGGL(k, dim3(blocks), dim3(64), 0, 0, dout, R, dcyc);
-    CK(hipDeviceSynchronize());
+  auto run = [&](int which, int blocks, int per) {
+    for (int rep = 0; rep < 2; ++rep) {
+      switch (which) {
+        case 0: hipLaunchKernelGGL(t4<1>, dim3(blocks), dim3(64), 0, 0, dout, R, dcyc); break;
+        case 1: hipLaunchKernelGGL(t4<4>, dim3(blocks), dim3(64), 0, 0, dout, R, dcyc); break;
+        case 2: hipLaunchKernelGGL(t4<8>, dim3(blocks), dim3(64), 0, 0, dout, R, dcyc); break;
+        case 3: hipLaunchKernelGGL(t16<1>, dim3(blocks), dim3(64), 0, 0, dout, R, dcyc); break;
+        default: hipLaunchKernelGGL(t16<4>, dim3(blocks), dim3(64), 0, 0, dout, R, dcyc); break;
+      }
+      CK(hipGetLastError());
+      CK(hipDeviceSynchronize());
+    }
     std::vector<long long> cy(blocks);
     CK(hipMemcpy(cy.data(), dcyc, 8 * blocks, hipMemcpyDeviceToHost));
     double s = 0;
@@ -213,7 +274,6 @@ int main() {
   printf(", \"cycles_per_mfma\": {\"f64_4x4x4_4b_dependent\": %.2f, \"f64_4x4x4_4b_4chains\": %.2f, "
          "\"f64_4x4x4_4b_8chains\": %.2f, \"f64_16x16x4_dependent\": %.2f, \"f64_16x16x4_4chains\": %.2f, "
          "\"f64_4x4x4_4b_4chains_2waves_per_simd\": %.2f, \"note\": \"clock64 cycles per instruction per wave\"}}\n",
-         run(t4<1>, 1024, 1), run(t4<4>, 1024, 4), run(t4<8>, 1024, 8), run(t16<1>, 1024, 1), run(t16<4>, 1024, 4),
-         run(t4<4>, 2048, 4));
+         run(0, 1024, 1), run(1, 1024, 4), run(2, 1024, 8), run(3, 1024, 1), run(4, 1024, 4), run(1, 2048, 4));
   return 0;
 }
