@@ -377,7 +377,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       }
     }
   };
-  auto stack_scalars = [&](int k, T& al, long long& nn, long long& nna) __attribute__((always_inline)) {
+  auto stack_scalars = [&](int k, T& al, int& nn, int& nna) __attribute__((always_inline)) {
     if (k < KL) {
       al = lalpha[k * CPB + cib];
       nn = lnn[k * CPB + cib];
@@ -472,12 +472,13 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   T qe[E], pe[E], ge[E];  // edge: the trajectory end on side v (being integrated)
   T qf[E], pf[E], gf[E];  // the far end
   int v = 1, j = 0;
-  long long l = 0, n = 1;
+  // tree counts fit 32 bits: the depth cap (<= NUTS_MAX_DEPTH_LIMIT = 30) bounds n by 2^30
+  int l = 0, n = 1;
   T joint0 = (T)0, logu = (T)0;
   uint64_t key = 0;
   uint32_t merge_ctr = 0;
   T fq[E], fp[E], pr[E];  // current subtree: first q, first p, proposal
-  long long tn = 0, tna = 0;
+  int tn = 0, tna = 0;
   bool ts = true;
   T ta = (T)0;
 #pragma unroll
@@ -598,7 +599,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
         // returns it unchanged; going up, it is merged wherever that parent
         // is itself a right child (the recursion's post-order).
         if (!ts) { ++k; continue; }
-        stack_store(k, fq, fp, pr, ta, (int)tn, (int)tna);
+        stack_store(k, fq, fp, pr, ta, tn, tna);
         break;
       }
       // right child: merge with the stored left sibling (:1251-1323)
@@ -608,11 +609,11 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       T lq[E], lpv[E];
       stack_vec(k, 0, lq);
       stack_vec(k, 1, lpv);
-      long long ln_, lna;
+      int ln_, lna;
       T lal;
       stack_scalars(k, lal, ln_, lna);
       const double u = nuts_u<double>(key, 64u + merge_ctr++);
-      const long long den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
+      const int den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
       if (!(u < (double)tn / (double)den)) stack_vec(k, 2, pr);
       tn = ln_ + tn;
       if (ts) ts = (v > 0) ? no_uturn<LPC, E>(lq, qe, lpv, pe) : no_uturn<LPC, E>(qe, lq, pe, lpv);
@@ -630,7 +631,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     // --- the doubling is complete (or truncated): top level (:785-880).
     // The new end on side v is the edge; alpha / n_alpha are this subtree's.
     const T alpha = ta;
-    const long long n_alpha = tna;
+    const int n_alpha = tna;
 #ifdef GM_NUTS_PROF
     f_dbl = true;
 #endif

@@ -18,6 +18,7 @@ for step in "$@"; do
     mfma) run mfma_probe 60 ./tools/probes/bin/gemv_mfma_probe 8192 200 ;;
     tests) run gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     mfmatest) run mfma_tests 300 python -u -m pytest tests/test_gpu_mfma_gauss.py -x -q --timeout 120 --timeout-method thread ;;
+    fixed) run hmc_fixed 120 python tools/probe_hmc_fixed.py ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) run bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench) run bench 300 python bench.py ;;
