@@ -340,10 +340,19 @@ def fin(v):
 
 
 def rhat_block(rhat):
+    """Both orientations, and Stan's over the parameters: the maximum is
+    parameter 0 on RosenbrockND, whose chains settle in the x0 = +1 or the
+    x0 = -1 basin and stay there (R-hat ~ 11 at any burn-in length,
+    tools/probe_ess_burnin.py); the median is the mixing of the rest."""
     r = np.asarray(rhat, dtype=np.float64)
     stan = 1.0 / r
+    ok = np.isfinite(stan)
+    q = (lambda p: fin(np.quantile(stan[ok], p))) if ok.any() else (lambda p: None)
     return {"reference_sqrt_W_over_V": {"min": fin(np.min(r)), "max": fin(np.max(r))},
-            "stan_sqrt_V_over_W": {"min": fin(np.min(stan)), "max": fin(np.max(stan))},
+            "stan_sqrt_V_over_W": {"min": fin(np.min(stan)), "max": fin(np.max(stan)),
+                                   "median": q(0.5), "p90": q(0.9),
+                                   "frac_below_1p01": float(np.mean(stan[ok] < 1.01)) if ok.any() else None,
+                                   "argmax": int(np.argmax(np.where(ok, stan, -np.inf))) if ok.any() else None},
             "max_abs_dev_from_1": fin(np.max(np.abs(stan - 1.0)))}
 
 
