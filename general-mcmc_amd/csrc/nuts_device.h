@@ -491,6 +491,11 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   unsigned long long ptop = __builtin_amdgcn_s_memtime();
   bool f_start = false, f_merge = false, f_dbl = false, f_trans = false;
 #endif
+  // Every load issued before the loop (state, step sizes, tracker) is
+  // complete here. On gfx9 stores count in vmcnt too: with a load still
+  // pending at the loop entry, the wait the compiler puts at the loop head
+  // would also wait out the previous transition's sample stores.
+  __builtin_amdgcn_s_waitcnt(0);
   while (true) {
     const bool live = s < a.n_steps;
 #ifdef GM_NUTS_PROF

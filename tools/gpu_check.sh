@@ -20,6 +20,7 @@ for step in "$@"; do
     mfmatest) run mfma_tests 300 python -u -m pytest tests/test_gpu_mfma_gauss.py -x -q --timeout 120 --timeout-method thread ;;
     fixed) run hmc_fixed 120 python tools/probe_hmc_fixed.py ;;
     essburn) run ess_burnin 300 python tools/probe_ess_burnin.py ;;
+    fixed2) run hmc_fixed2 120 python tools/probe_hmc_fixed2.py ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) run bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench) run bench 300 python bench.py ;;

@@ -12,8 +12,10 @@ in its own directory under PROF_DIR:
   grbm/   --pmc GRBM_GUI_ACTIVE       (GPU busy cycles of the dispatch, summed
                                        over the 8 XCDs)
 
-The timed launch is the bench's SECOND hmc_kernel dispatch (the first is the
-warm-up). Writes/updates profiles/r02/pmc_hmc.json under the shape key
+The timed launch is the bench's FOURTH hmc_kernel dispatch (--index 3: the
+W-transition warm-up, then the two device warm-up launches on a scratch
+sampler; --index 1 for profiles taken before the scratch warm-up existed).
+Writes/updates profiles/r02/pmc_hmc.json under the shape key
 C{chains}_D{dim}_L{L}_{dtype}, by_steps[K]; with two or more K profiled, also
 a linear fit bytes = fixed + K x per-transition, which bench.py uses for a K
 that was not profiled (marked scaled).
@@ -60,15 +62,17 @@ def main():
     ap.add_argument("--steps", type=int, required=True)
     ap.add_argument("--key", default="C4096_D64_L50_f32")
     ap.add_argument("--simds", type=int, default=1024)
+    ap.add_argument("--index", type=int, default=3, help="the timed launch's index among hmc_kernel dispatches")
     a = ap.parse_args()
-    dur = launch_seconds(os.path.join(a.prof_dir, "trace"))
-    f_kb = dispatch_counters(os.path.join(a.prof_dir, "fetch"))["FETCH_SIZE"]
-    w_kb = dispatch_counters(os.path.join(a.prof_dir, "write"))["WRITE_SIZE"]
-    sq = dispatch_counters(os.path.join(a.prof_dir, "sq"))
-    grbm = dispatch_counters(os.path.join(a.prof_dir, "grbm"))
+    ix = a.index
+    dur = launch_seconds(os.path.join(a.prof_dir, "trace"), index=ix)
+    f_kb = dispatch_counters(os.path.join(a.prof_dir, "fetch"), index=ix)["FETCH_SIZE"]
+    w_kb = dispatch_counters(os.path.join(a.prof_dir, "write"), index=ix)["WRITE_SIZE"]
+    sq = dispatch_counters(os.path.join(a.prof_dir, "sq"), index=ix)
+    grbm = dispatch_counters(os.path.join(a.prof_dir, "grbm"), index=ix)
     cycles = grbm["GRBM_GUI_ACTIVE"] / 8.0
     fdir = os.path.join(a.prof_dir, "flops")
-    fl = dispatch_counters(fdir) if os.path.isdir(fdir) else {}
+    fl = dispatch_counters(fdir, index=ix) if os.path.isdir(fdir) else {}
     entry = {
         "hbm_bytes_per_launch": (2 * f_kb + w_kb) * 1024.0,
         "fetch_size_kb": f_kb, "write_size_kb": w_kb,
@@ -84,7 +88,7 @@ def main():
         },
         "correction": "HBM bytes = FETCH_SIZE x 2 (gfx950 half count) + WRITE_SIZE, KB = 1024 B",
         "source": f"{a.prof_dir}: trace, fetch, write, sq, grbm passes (rocprofv3, one run each); "
-                  "the second hmc_kernel dispatch",
+                  f"hmc_kernel dispatch index {ix} (the timed launch)",
     }
     if fl:
         f32 = fl.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0)

@@ -32,7 +32,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prof_dir")
     ap.add_argument("--key", default="C4096_D64_L50_K100_f32")
-    ap.add_argument("--write", action="store_true", help="update profiles/pmc_traffic.json")
+    ap.add_argument("--write", action="store_true", help="update profiles/r01/pmc_traffic.json")
     a = ap.parse_args()
     fetch = counter_rows(os.path.join(a.prof_dir, "fetch"), "FETCH_SIZE")
     write = counter_rows(os.path.join(a.prof_dir, "write"), "WRITE_SIZE")
@@ -57,7 +57,7 @@ def main():
     }
     print(json.dumps({a.key: entry}, indent=1))
     if a.write:
-        p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        p = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
         d = json.load(open(p)) if os.path.exists(p) else {}
         d[a.key] = entry
         json.dump(d, open(p, "w"), indent=1)

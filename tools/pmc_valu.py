@@ -59,7 +59,7 @@ def main():
     }
     print(json.dumps({a.key: entry}, indent=1))
     if a.write:
-        p = os.path.join(ROOT, "profiles", "pmc_valu.json")
+        p = os.path.join(ROOT, "profiles", "r01", "pmc_valu.json")
         d = json.load(open(p)) if os.path.exists(p) else {}
         d[a.key] = entry
         json.dump(d, open(p, "w"), indent=1)
