@@ -21,6 +21,8 @@ for step in "$@"; do
     fixed) run hmc_fixed 120 python tools/probe_hmc_fixed.py ;;
     essburn) run ess_burnin 300 python tools/probe_ess_burnin.py ;;
     fixed2) run hmc_fixed2 120 python tools/probe_hmc_fixed2.py ;;
+    abhmc) run ab_hmc100 300 python tools/ab_run.py general-mcmc_amd/lib/libgmcmc.so $AB_LIBS &&
+           AB_ARGS="--layouts 64x1 --rounds 3 --steps 20" run ab_hmc20 300 python tools/ab_run.py general-mcmc_amd/lib/libgmcmc.so $AB_LIBS ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) run bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench) run bench 300 python bench.py ;;
