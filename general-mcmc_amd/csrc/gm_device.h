@@ -556,6 +556,9 @@ template <class T, int LPC, int E> struct GaussLane {
   const T* sprec;  // LDS [D][S], or the matrix-core fragments (mf), or null
   T* sd;           // LDS slot of this lane group's d [S] (mf: transposed [4][8])
   bool mf;         // matrix-core form (see above)
+#ifdef GM_NUTS_PROF
+  mutable unsigned long long prof_prod = 0;  // measurement build: cycles in mfma_product
+#endif
   // unreduced log-density term for callers that reduce it together with
   // another per-chain sum: logp = finish(group_sum(eval_part(...)))
   template <int LPC_> static constexpr bool has_part = true;
@@ -574,6 +577,9 @@ template <class T, int LPC, int E> struct GaussLane {
   __device__ __forceinline__ void mfma_product(const T (&d)[E], T (&w)[E]) const {
     if constexpr (GaussT<T>::template mfma_form<LPC, E>()) {
       typedef double v2 __attribute__((ext_vector_type(2)));
+#ifdef GM_NUTS_PROF
+      const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
+#endif
       const int l = threadIdx.x & 63;
       const int wb = (threadIdx.x >> 6) * 4;  // the wave's first chain slot in the block
       // the previous evaluation's reads of the slots are done before they are replaced
@@ -612,6 +618,10 @@ template <class T, int LPC, int E> struct GaussLane {
       const v2 wv = *(const v2*)(ws + (threadIdx.x >> 4) * 32 + (l & 15) * E);
       w[0] = wv[0];
       w[1] = wv[1];
+#ifdef GM_NUTS_PROF
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the product's last read has landed
+      prof_prod += __builtin_amdgcn_s_memtime() - pt0;
+#endif
     }
   }
   template <int LPC_, int E_, bool LOGP>

@@ -155,6 +155,7 @@ struct gm_sampler {
   std::vector<hipEvent_t> evs;
   double last_ms = 0;
   long long last_launches = 0;
+  bool last_ms_pending = false;  // HMC/MH: last_ms is read from evs[0..1] on request
   long long total_steps = 0;  // transitions since creation
   long long last_rows = 0;    // sample rows produced by the last run
   NutsState nuts;
@@ -580,6 +581,12 @@ int gm_sampler_reserve(gm_sampler* s, int64_t n_collect) {
 
 int gm_sampler_last_run_stats(gm_sampler* s, double* kernel_ms, int64_t* launches) {
   GM_REQ(s, "sampler is NULL");
+  if (s->last_ms_pending) {  // the run's event pair, read only when asked for (off the run's path)
+    float t = 0;
+    GM_HIP(hipEventElapsedTime(&t, s->evs[0], s->evs[1]));
+    s->last_ms = t;
+    s->last_ms_pending = false;
+  }
   if (kernel_ms) *kernel_ms = s->last_ms;
   if (launches) *launches = s->last_launches;
   return GM_OK;
@@ -630,6 +637,7 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
   GM_HIP(use_device(s->device));
   s->last_ms = 0;
   s->last_launches = 0;
+  s->last_ms_pending = false;
   // NUTS always launches: init_chain_state + row 0 even with zero transitions
   if (total <= 0 && s->kind != K_NUTS) return GM_OK;
   if (s->kind == K_NUTS) {
@@ -712,9 +720,7 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
   s->step += total;
   s->total_steps += total;
   GM_HIP(hipStreamSynchronize(s->stream));
-  float t = 0;
-  GM_HIP(hipEventElapsedTime(&t, s->evs[0], s->evs[1]));
-  s->last_ms = t;
+  s->last_ms_pending = true;
   s->last_launches = n_launch;
   return GM_OK;
 }

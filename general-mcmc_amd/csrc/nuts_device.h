@@ -301,7 +301,7 @@ __device__ __attribute__((noinline)) T find_reasonable_epsilon(const TG& tg, con
 // wave's chains did in it (bit 0 a transition start, 1 a subtree merge,
 // 2 a doubling end, 3 a transition end) plus the evaluation's share;
 // read back by gm_nuts_prof_read (nuts_kernels.hip).
-constexpr int NPROF_SLOTS = 16 * 2 + 2;
+constexpr int NPROF_SLOTS = 16 * 2 + 3;
 constexpr int NPROF_WAVES = 8192;
 __device__ unsigned long long gm_nuts_prof_buf[NPROF_WAVES * NPROF_SLOTS];
 #endif
@@ -732,6 +732,9 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       for (int b = 0; b < 16; ++b) { o[2 * b] = pcnt[b]; o[2 * b + 1] = pcyc[b]; }
       o[32] = peval;
       o[33] = piter;
+      unsigned long long pprod = 0;  // cycles inside the target's matrix-core product, if it has one
+      if constexpr (requires { tg.prof_prod; }) pprod = tg.prof_prod;
+      o[34] = pprod;
     }
   }
 #endif

@@ -29,7 +29,7 @@ for step in "$@"; do
     configs) run configs 300 python tools/bench_configs.py ;;
     mfma64) run mfma_f64_probe 60 ./tools/probes/bin/mfma_f64_probe ;;
     first)
-      for v in "--warm-collect" "--warm-collect --scratch-warm 1" "--warm-collect --scratch-warm 2" "--warm-collect" "--warm-collect --scratch-warm 1" "--warm-collect --scratch-warm 2"; do
+      for v in ${FIRST_VARIANTS:-"--warm-collect --scratch-warm 2" "--warm-collect --scratch-warm 2" "--warm-collect --scratch-warm 2"}; do
         run first_call 60 python tools/probe_bench_first.py --repeat 4 $v && cat gpurun_out/first_call.log >> gpurun_out/first_calls.jsonl
       done ;;
     nprof) run nuts_prof 120 env GMCMC_LIB=abtest/nprof/libgmcmc.so python tools/probe_nuts_prof.py ;;

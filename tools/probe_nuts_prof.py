@@ -36,7 +36,7 @@ def main():
     lib = gm._lib.load()
     lanes, elems = s.layout()
     waves = chains * lanes // 64
-    buf = np.zeros((waves, 34), np.uint64)
+    buf = np.zeros((waves, 35), np.uint64)
     f = lib.gm_nuts_prof_read
     f.argtypes = [C.c_void_p, C.c_longlong]
     assert f(buf.ctypes.data, buf.size) == 0
@@ -46,7 +46,8 @@ def main():
     out = {"chains": chains, "layout": f"{lanes}x{elems}", "waves": waves, "leapfrogs": lf,
            "iterations_per_wave": it / waves, "leapfrogs_per_chain": lf / chains,
            "cycles_per_iteration": float(cyc.sum() / it),
-           "eval_cycles_per_iteration": float(buf[:, 32].astype(np.float64).sum() / it), "bins": []}
+           "eval_cycles_per_iteration": float(buf[:, 32].astype(np.float64).sum() / it),
+           "product_cycles_per_iteration": float(buf[:, 34].astype(np.float64).sum() / it), "bins": []}
     for b in range(16):
         if cnt[b] == 0:
             continue
