@@ -13,7 +13,7 @@
 // (the reference's f32 ndarray sums are what the 1e-3 tolerance absorbs).
 //
 // Three stages so that the multi-GPU path can all-gather the middle products:
-//   series_gram_kernel (h <= 64; MFMA) / series_kernel (any h):
+//   series_gram_kernel (h <= 64; MFMA) / series_lag_kernel (h > 64):
 //                  per split chain k and parameter p -> cm, s2 ([P][2C]), and
 //                  acov summed over a chain group's split chains ([G][h][P])
 //   acov_reduce_kernel: partials -> acov_sum[l][p] in fixed group order
@@ -29,62 +29,115 @@ __device__ __forceinline__ float load_f32(const T* base, long long idx) {
   return (float)base[idx];
 }
 
-// blockDim.x = PT * KB: PT parameters (fastest) x KB split chains.
-// Dynamic LDS: h * blockDim.x floats (the block's series, t-major) when use_lds.
+// ---------------------------------------------------------------------------
+// series_lag_kernel: the same products for h > 64 (long runs), one wave per
+// parameter. Block = LT_PT waves = LT_PT consecutive parameters x one chain
+// group; the block walks the group's split chains: it stages a split chain's
+// h draws of its LT_PT parameters in LDS (rounded to f32 as the reference
+// does), each wave centres its parameter's series (mean and within-variance
+// by wave reduction, written to cm/s2), and then accumulates the lagged
+// products of a block of 512 lags over all t: lane l owns lags
+// L0 + 8l + j (j < 8) and keeps the 8 values y~[t + L0 + 8l + j] as a sliding
+// register window, so one step of t costs one broadcast read of y~[t], one
+// new window read and 8 f64 fma. Series are stored skewed (element i at
+// i + i/8) so that the window reads of a wave (8 elements apart) hit distinct
+// banks, and zero-padded past h so that no lane tests bounds. The group's sums
+// stay in registers across its chains; acov_part[g][l][p] = sum / h. Lags
+// beyond 512 take further passes over the group (h > 512 only).
+constexpr int LT_PT = 8;                // parameters (waves) per block
+constexpr int LT_T = LT_PT * 64;        // threads per block
+constexpr int LT_LAGS = 512;            // lags per pass (64 lanes x 8)
+__host__ __device__ constexpr int lt_skew(int i) { return i + (i >> 3); }
+__host__ __device__ constexpr int lt_stride(int h) { return lt_skew(h + LT_LAGS + 8) + 1; }
+
 template <class T>
-__global__ void series_kernel(const T* __restrict__ x, long long C, long long N, long long P,
-                              long long sc, long long sd, long long sp, int h, int PT, int KB,
-                              int use_lds, double* __restrict__ cm, double* __restrict__ s2,
-                              double* __restrict__ acov_part /* [G][h][P] */) {
-  extern __shared__ float lds[];
-  const int tid = threadIdx.x;
-  const int pt = tid % PT, kb = tid / PT;
-  const long long nPB = (P + PT - 1) / PT;
-  const long long p = (long long)(blockIdx.x % nPB) * PT + pt;
-  const long long g = blockIdx.x / nPB;  // chain group
-  const long long k = g * KB + kb; // split-chain index in [0, 2C)
-  const bool valid = (p < P) && (k < 2 * C);
-  const long long chain = valid ? (k < C ? k : k - C) : 0;
-  const long long t0 = (k < C) ? 0 : N - h;
-  const T* __restrict__ base = x + chain * sc + (valid ? p : 0) * sp;
-  const int nth = blockDim.x;
-  // pass 1: load to LDS (or not) and the mean
-  double sum = 0.0;
-  for (int t = 0; t < h; ++t) {
-    const float y = valid ? load_f32(base, (t0 + t) * sd) : 0.0f;
-    if (use_lds) lds[t * nth + tid] = y;
-    sum += (double)y;
-  }
-  const double mean = valid ? sum / (double)h : 0.0;
-  auto Y = [&](int t) -> double {
-    const float y = use_lds ? lds[t * nth + tid] : (valid ? load_f32(base, (t0 + t) * sd) : 0.0f);
-    return (double)y - mean;
-  };
-  double sq = 0.0;
-  for (int t = 0; t < h; ++t) {
-    const double d = Y(t);
-    sq += d * d;
-  }
-  if (valid) {
-    cm[p * 2 * C + k] = mean;
-    s2[p * 2 * C + k] = sq / (double)h;
-  }
-  __syncthreads();  // all series loaded before LDS is reused below
-  // autocovariance, summed over the KB chains of this block for each (l, p)
-  double* red = (double*)(lds + (use_lds ? (long long)h * nth : 0));
-  for (int l = 0; l < h; ++l) {
-    double acc = 0.0;
-    for (int t = 0; t + l < h; ++t) acc += Y(t) * Y(t + l);
-    acc = valid ? acc / (double)h : 0.0;
-    // reduce over kb for the same pt (fixed tree order)
-    red[tid] = acc;
-    __syncthreads();
-    for (int w = KB / 2; w >= 1; w >>= 1) {
-      if (kb < w) red[tid] = red[tid] + red[tid + w * PT];
+__global__ __launch_bounds__(LT_T) void series_lag_kernel(const T* __restrict__ x, long long C, long long N,
+                                                          long long P, long long sc, long long sd, long long sp,
+                                                          int h, long long nPT, long long KPG,
+                                                          double* __restrict__ cm, double* __restrict__ s2,
+                                                          double* __restrict__ acov_part /* [G][h][P] */) {
+  extern __shared__ float ys[];  // [LT_PT][stride] skewed series
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long pt0 = (long long)(blockIdx.x % nPT) * LT_PT;
+  const long long g = blockIdx.x / nPT;
+  const long long p = pt0 + w;
+  const bool pvalid = p < P;
+  const int stride = lt_stride(h);
+  float* my = ys + w * stride;
+  const long long k0 = g * KPG, k1 = (k0 + KPG < 2 * C) ? k0 + KPG : 2 * C;
+  // zero the padding once (the series part is rewritten for every chain)
+  for (int i = h + lane; i < h + LT_LAGS + 8; i += 64) my[lt_skew(i)] = 0.0f;
+  for (int L0 = 0; L0 < h; L0 += LT_LAGS) {
+    double acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.0;
+    for (long long k = k0; k < k1; ++k) {
+      const long long chain = k < C ? k : k - C;
+      const long long t0 = k < C ? 0 : N - h;
+      __syncthreads();  // the previous series is no longer read
+      // stage: consecutive threads take consecutive parameters of one draw
+      for (int i = tid; i < h * LT_PT; i += LT_T) {
+        const int t = i / LT_PT, q = i - t * LT_PT;
+        const long long pq = pt0 + q;
+        ys[q * stride + lt_skew(t)] = pq < P ? load_f32(x + chain * sc + pq * sp, (t0 + t) * sd) : 0.0f;
+      }
       __syncthreads();
+      // centre (in f64, rounded back to f32 in LDS) and, on the first pass,
+      // the split chain's mean and within-variance
+      double sum = 0.0;
+      for (int t = lane; t < h; t += 64) sum += (double)my[lt_skew(t)];
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
+      const double mean = sum / (double)h;
+      double sq = 0.0;
+      for (int t = lane; t < h; t += 64) {
+        const double d = (double)my[lt_skew(t)] - mean;
+        sq += d * d;
+        my[lt_skew(t)] = (float)d;
+      }
+      if (L0 == 0) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) sq += __shfl_xor(sq, o);
+        if (pvalid && lane == 0) {
+          cm[p * 2 * C + k] = mean;
+          s2[p * 2 * C + k] = sq / (double)h;
+        }
+      }
+      // this wave's own series: its writes above are visible to its reads below
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int base = L0 + 8 * lane;  // this lane's first lag
+      double win[8];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) win[j] = (double)my[lt_skew(base + j)];
+      const int tn = h - L0;  // t past which every lag of this pass reads padding
+      int t = 0;
+      for (; t + 8 <= tn; t += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          // window slot (u + 7) % 8 takes y~[t + u + base + 7]
+          win[(u + 7) & 7] = (double)my[lt_skew(t + u + base + 7)];
+          const double a = (double)my[lt_skew(t + u)];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] = __builtin_fma(a, win[(u + j) & 7], acc[j]);
+        }
+      }
+      for (; t < tn; ++t) {  // the tail, window kept in order
+        win[7] = (double)my[lt_skew(t + base + 7)];
+        const double a = (double)my[lt_skew(t)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = __builtin_fma(a, win[j], acc[j]);
+#pragma unroll
+        for (int j = 0; j < 7; ++j) win[j] = win[j + 1];
+      }
     }
-    if (kb == 0 && p < P) acov_part[(g * h + l) * P + p] = red[tid];
-    __syncthreads();
+    if (pvalid) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int l = L0 + 8 * lane + j;
+        if (l < h) acov_part[(g * h + l) * P + p] = acc[j] / (double)h;
+      }
+    }
   }
 }
 
@@ -358,35 +411,30 @@ int diag_series(gm_dtype dt, const void* x, long long C, long long N, long long 
                          C, N, P, sc, sd, sp, h, (int)nPT, CPG, cm, s2, (double*)ws.part);
     e = hipGetLastError();
   } else {
-    int PT = 1;
-    while (PT < P && PT < 16) PT <<= 1;
-    int nth;
-    int use_lds = 1;
-    if ((long long)h * 256 * 4 + 256 * 8 <= 150 * 1024) nth = 256;
-    else if ((long long)h * 128 * 4 + 128 * 8 <= 150 * 1024) nth = 128;
-    else if ((long long)h * 64 * 4 + 64 * 8 <= 150 * 1024) nth = 64;
-    else {
-      nth = 256;
-      use_lds = 0;
-    }
-    if (nth < PT) nth = PT;
-    const int KB = nth / PT;
-    G = (2 * C + KB - 1) / KB;
-    int rc = ensure_part((size_t)G * h * P * sizeof(double));
-    if (rc) return rc;
-    const size_t lds = (use_lds ? (size_t)h * nth * 4 : 0) + (size_t)nth * 8;
-    const long long nblk = ((P + PT - 1) / PT) * G;
-    if (nblk > 0x7fffffffLL) {
+    // long series: ~512 blocks of LT_PT waves over chain groups of split chains
+    const long long nPT = (P + LT_PT - 1) / LT_PT;
+    G = (512 + nPT - 1) / nPT;
+    if (G > 2 * C) G = 2 * C;
+    const long long KPG = (2 * C + G - 1) / G;
+    G = (2 * C + KPG - 1) / KPG;
+    if (nPT * G > 0x7fffffffLL) {
       set_error("diagnostics: problem too large for one launch");
       return GM_EINVAL;
     }
-    dim3 grid((unsigned)nblk);
+    int rc = ensure_part((size_t)G * h * P * sizeof(double));
+    if (rc) return rc;
+    const size_t lds = (size_t)LT_PT * lt_stride(h) * sizeof(float);
+    if (lds > 160 * 1024) {
+      set_error("diagnostics: series too long for the LDS staging (h > ~4500)");
+      return GM_EINVAL;
+    }
+    dim3 grid((unsigned)(nPT * G));
     if (dt == GM_F32)
-      hipLaunchKernelGGL(series_kernel<float>, grid, dim3(nth), lds, st, (const float*)x, C, N, P, sc,
-                         sd, sp, h, PT, KB, use_lds, cm, s2, (double*)ws.part);
+      hipLaunchKernelGGL(series_lag_kernel<float>, grid, dim3(LT_T), lds, st, (const float*)x, C, N, P, sc,
+                         sd, sp, h, nPT, KPG, cm, s2, (double*)ws.part);
     else
-      hipLaunchKernelGGL(series_kernel<double>, grid, dim3(nth), lds, st, (const double*)x, C, N, P,
-                         sc, sd, sp, h, PT, KB, use_lds, cm, s2, (double*)ws.part);
+      hipLaunchKernelGGL(series_lag_kernel<double>, grid, dim3(LT_T), lds, st, (const double*)x, C, N, P,
+                         sc, sd, sp, h, nPT, KPG, cm, s2, (double*)ws.part);
     e = hipGetLastError();
   }
   if (e != hipSuccess) {
