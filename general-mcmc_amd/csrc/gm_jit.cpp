@@ -69,7 +69,7 @@ std::string name_expr(JitKernel which, gm_dtype dt, int D) {
   // the NUTS kernel's last argument: metric handling compiled in (user
   // targets run with or without mass-matrix adaptation from one module)
   return std::string("gm::") + kKernelName[which] + "<" + t + ", 1, " + std::to_string(D) +
-         ", gm::UserTarget<" + t + ">" + (which == JIT_NUTS ? ", true" : "") + " >";
+         ", gm::UserTarget<" + t + ">" + (which == JIT_NUTS ? ", 2" : "") + " >";
 }
 
 // compile; on success fills code and the lowered kernel name

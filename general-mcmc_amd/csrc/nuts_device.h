@@ -20,28 +20,31 @@ __device__ __forceinline__ T coord(const T (&x)[E], int j) {
   else return __shfl(mine, src, LPC);
 }
 
-// MassMatrix (generic_nuts.rs:175-304) of one chain, this lane's view. DYN
-// false: the identity metric known at compile time (a sampler without
-// mass-matrix adaptation), so no metric branch is ever emitted.
-template <class T, int E, bool DYN = true> struct MassDev {
+// MassMatrix (generic_nuts.rs:175-304) of one chain, this lane's view. K is
+// the most general metric the kernel supports, known at compile time: 0 the
+// identity only (a sampler without mass-matrix adaptation: no metric branch
+// is emitted), 1 identity or diagonal (diagonal adaptation: no dense code),
+// 2 any (dense adaptation).
+template <class T, int E, int K = 2> struct MassDev {
+  static constexpr bool DENSE = K >= 2;
   int kind_ = 0;            // 0 identity, 1 diagonal, 2 dense
   T inv[E], sq[E];          // diagonal
   const T* minv = nullptr;  // dense [D][D]
   const T* chol = nullptr;
   int D = 0;
   __device__ __forceinline__ int kind() const {
-    if constexpr (DYN) return kind_;
+    if constexpr (K > 0) return kind_;
     else return 0;
   }
 };
 
 // inv_mul (:255-273): v = M^-1 p
-template <int LPC, int E, class T, bool DYN>
-__device__ __forceinline__ void inv_mul(const MassDev<T, E, DYN>& M, const T (&p)[E], T (&v)[E], int lane) {
+template <int LPC, int E, class T, int K>
+__device__ __forceinline__ void inv_mul(const MassDev<T, E, K>& M, const T (&p)[E], T (&v)[E], int lane) {
   if (M.kind() == 1) {
 #pragma unroll
     for (int e = 0; e < E; ++e) v[e] = M.inv[e] * p[e];
-  } else if (M.kind() == 2) {
+  } else if (MassDev<T, E, K>::DENSE && M.kind() == 2) {
     T acc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
@@ -62,12 +65,12 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E, DYN>& M, const T (&p
 }
 
 // sample_momentum (:275-303) applied to standard normals z
-template <int LPC, int E, class T, bool DYN>
-__device__ __forceinline__ void momentum_from(const MassDev<T, E, DYN>& M, const T (&z)[E], T (&p)[E], int lane) {
+template <int LPC, int E, class T, int K>
+__device__ __forceinline__ void momentum_from(const MassDev<T, E, K>& M, const T (&z)[E], T (&p)[E], int lane) {
   if (M.kind() == 1) {
 #pragma unroll
     for (int e = 0; e < E; ++e) p[e] = z[e] * M.sq[e];
-  } else if (M.kind() == 2) {
+  } else if (MassDev<T, E, K>::DENSE && M.kind() == 2) {
     T acc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
@@ -138,8 +141,8 @@ __device__ __forceinline__ bool no_uturn(const T (&qm)[E], const T (&qp)[E], con
 
 // MassMatrix::kinetic (:226-253), canonical-order sum of the per-coordinate
 // terms p*p*inv (diagonal) or p_i (M^-1 p)_i (dense)
-template <int LPC, int E, class T, bool DYN>
-__device__ __forceinline__ T kinetic_m(const MassDev<T, E, DYN>& M, const T (&p)[E], int lane) {
+template <int LPC, int E, class T, int K>
+__device__ __forceinline__ T kinetic_m(const MassDev<T, E, K>& M, const T (&p)[E], int lane) {
   if (M.kind() == 0) return kinetic<LPC, E>(p);
   T t[E];
   if (M.kind() == 1) {
@@ -157,8 +160,8 @@ __device__ __forceinline__ T kinetic_m(const MassDev<T, E, DYN>& M, const T (&p)
 }
 
 // leapfrog_with_mass (:1396-1418): drift by M^-1 p
-template <int LPC, int E, class T, class TG, bool DYN>
-__device__ __forceinline__ T leapfrog_m(const TG& tg, const MassDev<T, E, DYN>& M, T (&q)[E], T (&p)[E],
+template <int LPC, int E, class T, class TG, int K>
+__device__ __forceinline__ T leapfrog_m(const TG& tg, const MassDev<T, E, K>& M, T (&q)[E], T (&p)[E],
                                         T (&g)[E], T epsv, int lane) {
   if (M.kind() == 0) return leapfrog<LPC, E>(tg, q, p, g, epsv, lane);
   const T h = epsv * (T)0.5;
@@ -177,8 +180,8 @@ __device__ __forceinline__ T leapfrog_m(const TG& tg, const MassDev<T, E, DYN>& 
 // Unreduced per-lane term of MassMatrix::kinetic (:226-253) without the
 // 0.5: sum_e p_e^2 (identity), p_e^2 inv_e (diagonal), p_e (M^-1 p)_e
 // (dense); kinetic = 0.5 * group_sum(part), the operations of kinetic_m.
-template <int LPC, int E, class T, bool DYN>
-__device__ __forceinline__ T kin_part_m(const MassDev<T, E, DYN>& M, const T (&p)[E], int lane) {
+template <int LPC, int E, class T, int K>
+__device__ __forceinline__ T kin_part_m(const MassDev<T, E, K>& M, const T (&p)[E], int lane) {
   T t[E];
   if (M.kind() == 0) {
 #pragma unroll
@@ -198,8 +201,8 @@ __device__ __forceinline__ T kin_part_m(const MassDev<T, E, DYN>& M, const T (&p
 }
 
 // stop_criterion_with_mass (:1354-1378), the top-level U-turn
-template <int LPC, int E, class T, bool DYN>
-__device__ __forceinline__ bool no_uturn_m(const MassDev<T, E, DYN>& M, const T (&qm)[E], const T (&qp)[E],
+template <int LPC, int E, class T, int K>
+__device__ __forceinline__ bool no_uturn_m(const MassDev<T, E, K>& M, const T (&qm)[E], const T (&qp)[E],
                                            const T (&pm)[E], const T (&pp)[E], int lane) {
   if (M.kind() == 0) return no_uturn<LPC, E>(qm, qp, pm, pp);
   T d[E], vm[E], vp[E];
@@ -306,7 +309,7 @@ constexpr int NPROF_WAVES = 8192;
 __device__ unsigned long long gm_nuts_prof_buf[NPROF_WAVES * NPROF_SLOTS];
 #endif
 
-template <class T, int LPC, int E, class TG, bool MASS>
+template <class T, int LPC, int E, class TG, int MASS>
 __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
@@ -414,7 +417,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       rmean[e] = (i < D) ? ((const T*)a.rmean)[c * D + i] : (T)0;
       rm2d[e] = (i < D) ? ((const T*)a.rm2d)[c * D + i] : (T)0;
     }
-    if (a.mass_mode == 2) {
+    if (MASS == 2 && a.mass_mode == 2) {
       M.minv = (const T*)a.minv + (long long)c * D * D;
       M.chol = (const T*)a.mchol + (long long)c * D * D;
     }
@@ -430,7 +433,12 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     }
     momentum_from<LPC, E>(M, z, p0, lane);
     const T ae = eps + (T)1;
-    if ((ae < (T)0 ? -ae : ae) <= MachEps<T>::v) eps = find_reasonable_epsilon<LPC, E>(tg, q, p0, lane, D);
+    // copies: the out-of-line search takes its arrays by address, which would
+    // otherwise keep the loop's q and momentum in scratch memory
+    T qc[E], pc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) { qc[e] = q[e]; pc[e] = p0[e]; }
+    if ((ae < (T)0 ? -ae : ae) <= MachEps<T>::v) eps = find_reasonable_epsilon<LPC, E>(tg, qc, pc, lane, D);
     mu = glog((T)10 * eps);
   }
   if (a.do_refind && a.updated[c]) {  // after a metric update (generic_nuts.rs:905-918)
@@ -441,7 +449,10 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       z[e] = (i < D) ? normal<T>(a.seed, cid, a.refind_step, TAG_NUTS_PROBE, (uint32_t)i) : (T)0;
     }
     momentum_from<LPC, E>(M, z, probe, lane);
-    eps = find_reasonable_epsilon<LPC, E>(tg, q, probe, lane, D);  // identity-mass leapfrog (:1009-1023)
+    T qc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) qc[e] = q[e];
+    eps = find_reasonable_epsilon<LPC, E>(tg, qc, probe, lane, D);  // identity-mass leapfrog (:1009-1023)
     mu = glog((T)10 * eps);
     eps_bar = eps;
     h_bar = (T)0;
@@ -704,7 +715,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
           d2[e] = q[e] - rmean[e];
           rm2d[e] = rm2d[e] + d1[e] * d2[e];
         }
-        if (a.mass_mode == 2) {
+        if (MASS == 2 && a.mass_mode == 2) {
           T* m2 = (T*)a.rm2 + (long long)c * D * D;
           for (int jj = 0; jj < D; ++jj) {
             const T dj = coord<LPC, E>(d2, jj);

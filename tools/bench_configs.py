@@ -41,6 +41,8 @@ def timed(fn):
 def cfg3(a):
     C, D = a.nuts_chains, 32
     s = gm.NUTS(dense_gauss_32(), gm.init_det(C, D), 0.8, dtype=np.float64, max_depth=10).set_seed(42)
+    if a.nuts_mass != "none":  # GenericNUTS::new_with_mass_matrix's warm-up metric adaptation
+        s.set_mass_adaptation(gm.NUTSMassMatrixConfig(a.nuts_mass))
     if a.nuts_layout:
         s.set_layout(*[int(v) for v in a.nuts_layout.split("x")])
     # warm-up (step-size adaptation) then sampling, as NUTS::run_progress
@@ -51,6 +53,7 @@ def cfg3(a):
     rhat, ess = ds.split_rhat_ess()
     eps, _ = s.step_sizes()
     return {"config": "cfg3 NUTS DenseGaussian32 f64", "chains": C, "layout": "%dx%d" % s.layout(),
+            "mass_adaptation": a.nuts_mass,
             "warmup_s": tw, "sample_s": ts, "leapfrogs": int(lf), "leapfrog_per_s": lf / ts,
             "mean_tree_leapfrogs": lf / (C * a.nuts_collect), "eps_median": float(np.median(eps)),
             "ess_mean": float(ess.mean()), "ess_min": float(ess.min()), "rhat_max": float(rhat.max()),
@@ -101,6 +104,8 @@ def ref10k(a):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--which", default="3,4,5,10k")
+    p.add_argument("--nuts-mass", default="none", choices=["none", "diagonal", "dense"],
+                   help="cfg3 with the warm-up metric adaptation (new_with_mass_matrix)")
     p.add_argument("--nuts-chains", type=int, default=8192)
     p.add_argument("--nuts-discard", type=int, default=500)
     p.add_argument("--nuts-collect", type=int, default=500)
