@@ -29,8 +29,8 @@ template <class T, int E, int K = 2> struct MassDev {
   static constexpr bool DENSE = K >= 2;
   int kind_ = 0;            // 0 identity, 1 diagonal, 2 dense
   T inv[E], sq[E];          // diagonal
-  const T* minv = nullptr;  // dense [D][D]
-  const T* chol = nullptr;
+  const T* minvT = nullptr;  // dense M^-1, transposed: minvT[j][i] = M^-1_ij (nuts_run)
+  const T* cholT = nullptr;  // its Cholesky factor L, transposed: cholT[j][i] = L_ij
   int D = 0;
   __device__ __forceinline__ int kind() const {
     if constexpr (K > 0) return kind_;
@@ -48,12 +48,28 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E, K>& M, const T (&p)[
     T acc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
-    for (int j = 0; j < M.D; ++j) {
-      const T pj = coord<LPC, E>(p, j);
+    // columns in batches of 8: a batch's loads and broadcasts are issued
+    // together (a runtime-trip loop around the shuffles is not unrolled by the
+    // compiler); the sums stay in ascending j
+    for (int j0 = 0; j0 < M.D; j0 += 8) {
+      T mv[8][E], pv[8];
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int i = lane * E + e;
-        if (i < M.D) acc[e] = acc[e] + M.minv[(long long)i * M.D + j] * pj;
+      for (int u = 0; u < 8; ++u) {
+        const int j = (j0 + u < M.D) ? j0 + u : M.D - 1;
+        pv[u] = coord<LPC, E>(p, j);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = lane * E + e;
+          mv[u][e] = (i < M.D) ? M.minvT[(long long)j * M.D + i] : (T)0;  // a chain's lanes: one row
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (j0 + u < M.D) {
+#pragma unroll
+          for (int e = 0; e < E; ++e)
+            if (lane * E + e < M.D) acc[e] = acc[e] + mv[u][e] * pv[u];
+        }
       }
     }
 #pragma unroll
@@ -74,12 +90,28 @@ __device__ __forceinline__ void momentum_from(const MassDev<T, E, K>& M, const T
     T acc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
-    for (int j = 0; j < M.D; ++j) {
-      const T zj = coord<LPC, E>(z, j);
+    for (int j0 = 0; j0 < M.D; j0 += 8) {  // batches of 8 columns, as inv_mul
+      T mv[8][E], zv[8];
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int i = lane * E + e;
-        if (i < M.D && j <= i) acc[e] = acc[e] + M.chol[(long long)i * M.D + j] * zj;
+      for (int u = 0; u < 8; ++u) {
+        const int j = (j0 + u < M.D) ? j0 + u : M.D - 1;
+        zv[u] = coord<LPC, E>(z, j);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = lane * E + e;
+          mv[u][e] = (i < M.D) ? M.cholT[(long long)j * M.D + i] : (T)0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u;
+        if (j < M.D) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const int i = lane * E + e;
+            if (i < M.D && j <= i) acc[e] = acc[e] + mv[u][e] * zv[u];
+          }
+        }
       }
     }
 #pragma unroll
@@ -418,8 +450,8 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       rm2d[e] = (i < D) ? ((const T*)a.rm2d)[c * D + i] : (T)0;
     }
     if (MASS == 2 && a.mass_mode == 2) {
-      M.minv = (const T*)a.minv + (long long)c * D * D;
-      M.chol = (const T*)a.mchol + (long long)c * D * D;
+      M.minvT = (const T*)a.minv + (long long)c * D * D;
+      M.cholT = (const T*)a.mchol + (long long)c * D * D;
     }
     rn = a.rn[c];
   }

@@ -165,6 +165,20 @@ __global__ void nuts_fill_kernel(T* eps, T* eps_bar, T* h_bar, T* mu, long long 
   mu[i] = glog((T)10 * (T)1);       // :644
 }
 
+// [C][D][D] -> per-chain transposes (the sampling kernel reads a chain's
+// dense metric column by column: with the transpose, the chain's lanes read
+// one contiguous row per column instead of one cache line each)
+template <class T>
+__global__ void mat_transpose_kernel(long long C, int D, const T* __restrict__ in, T* __restrict__ out) {
+  const long long dd = (long long)D * D, n = C * dd;
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+       k += (long long)gridDim.x * blockDim.x) {
+    const long long c = k / dd;
+    const int r = (int)(k - c * dd), i = r / D, j = r - i * D;
+    out[c * dd + (long long)j * D + i] = in[k];
+  }
+}
+
 int nuts_init_state(NutsState* ns, gm_dtype dt, long long C, int D, int max_depth) {
   const size_t esz = dt == GM_F32 ? 4 : 8;
   ns->max_depth = max_depth;
@@ -430,6 +444,26 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
       a.dsq = ns.dsq;
       a.minv = ns.minv;
       a.mchol = ns.mchol;
+      if (ns.mass_mode == 2) {  // the transposes, in the update kernel's scratch (free between its launches)
+        const size_t esz = dt == GM_F32 ? 4 : 8, cdd = (size_t)C * D * D * esz;
+        void* mT = ns.mscratch;
+        void* lT = (char*)ns.mscratch + cdd;
+        const long long n = C * (long long)D * D;
+        const unsigned tb = (unsigned)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+        if (dt == GM_F32) {
+          hipLaunchKernelGGL(mat_transpose_kernel<float>, dim3(tb), dim3(256), 0, st, C, D, (const float*)ns.minv,
+                             (float*)mT);
+          hipLaunchKernelGGL(mat_transpose_kernel<float>, dim3(tb), dim3(256), 0, st, C, D,
+                             (const float*)ns.mchol, (float*)lT);
+        } else {
+          hipLaunchKernelGGL(mat_transpose_kernel<double>, dim3(tb), dim3(256), 0, st, C, D,
+                             (const double*)ns.minv, (double*)mT);
+          hipLaunchKernelGGL(mat_transpose_kernel<double>, dim3(tb), dim3(256), 0, st, C, D,
+                             (const double*)ns.mchol, (double*)lT);
+        }
+        a.minv = mT;
+        a.mchol = lT;
+      }
       a.rn = ns.rn;
       a.rmean = ns.rmean;
       a.rm2d = ns.rm2d;
