@@ -379,17 +379,19 @@ def main(argv=None, backend=None):
     # the sample buffer is resident before the clock starts, like the state;
     # the W warm-up transitions collect into it (untimed)
     sampler.reserve(max(a.steps, a.warmup))
-    if a.warmup > 0:
-        sampler.run_positions(a.warmup, 0)
     # device warm-up (untimed): two launches of the timed shape on a scratch
-    # sampler with its own chains and buffers. After a short warm-up the first
-    # launch of a process is ~10 us slower end to end than the ones after it
-    # (tools/probe_bench_first.py, profiles/r02/first_call/); the measured
-    # chains are still exactly W transitions from the start.
+    # sampler with its own chains and buffers, then the W warm-up transitions
+    # of the measured sampler right before the timed call. Without the scratch
+    # launches the first timed call of a process is ~10 us slower end to end
+    # than the ones after it, and with them placed after the W transitions it
+    # still is (tools/probe_bench_first.py, profiles/r02/first_call/). The
+    # measured chains are exactly W transitions from the start.
     scratch = be.sampler(x0, offset)
     scratch.reserve(a.steps)
     for _ in range(2):
         scratch.run_positions(a.steps, 0)
+    if a.warmup > 0:
+        sampler.run_positions(a.warmup, 0)
     barrier_sync()
     t0 = time.perf_counter()
     ds = sampler.run_positions(a.steps, 0)
@@ -468,8 +470,8 @@ def main(argv=None, backend=None):
                        "layout": f"{lanes}x{elems}", "parallelism": f"chains sharded x{world}"},
             "timing": {"wall_ms": t_max * 1e3, "kernel_ms": kmax, "launches": launches,
                        "host_overhead_ms": t_max * 1e3 - kmax, "per_rank": ranks,
-                       "device_warmup": "W transitions on the measured sampler, then two untimed launches of the "
-                                        "timed shape on a scratch sampler (own chains and buffers)",
+                       "device_warmup": "two untimed launches of the timed shape on a scratch sampler (own chains "
+                                        "and buffers), then the W warm-up transitions of the measured sampler",
                        "note": "wall = barrier-bracketed timed region (max over ranks); kernel = HIP events "
                                "around the run's launches on the sampler's stream; host_overhead = wall - kernel"},
             "ess_per_sec": legs.get("cfg2_schedule", {}).get("ess_per_sec_sampling"),

@@ -12,9 +12,10 @@ in its own directory under PROF_DIR:
   grbm/   --pmc GRBM_GUI_ACTIVE       (GPU busy cycles of the dispatch, summed
                                        over the 8 XCDs)
 
-The timed launch is the bench's FOURTH hmc_kernel dispatch (--index 3: the
-W-transition warm-up, then the two device warm-up launches on a scratch
-sampler; --index 1 for profiles taken before the scratch warm-up existed).
+The timed launch is the bench's FOURTH hmc_kernel dispatch (--index 3: two
+device warm-up launches on a scratch sampler and the W-transition warm-up
+come first, in either order; --index 1 for profiles taken before the scratch
+warm-up existed).
 Writes/updates profiles/r02/pmc_hmc.json under the shape key
 C{chains}_D{dim}_L{L}_{dtype}, by_steps[K]; with two or more K profiled, also
 a linear fit bytes = fixed + K x per-transition, which bench.py uses for a K
