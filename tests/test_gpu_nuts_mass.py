@@ -83,6 +83,23 @@ def test_dense_warmup_wide_layout(gm, oracle):
                    initial_window=10)
 
 
+def test_dense_warmup_matrix_core_layout(gm, oracle):
+    """D = 20 f64 runs at 16 lanes x 2 (the dense Gaussian's product on the
+    matrix cores), with the dense metric's transposed per-chain matrices and
+    column batches (20 = 8 + 8 + 4); 10 chains leave the last wave half
+    empty (the VALU product there)."""
+    rng = np.random.default_rng(21)
+    D = 20
+    a = rng.standard_normal((D, D))
+    cov = a @ a.T / D + 0.5 * np.eye(D)
+    t = _gauss(gm, cov, rng.standard_normal(D))
+    x0 = gm.init_with_seed(10, D, 6, np.float64)
+    s, om = _check_run(gm, oracle, t, x0, np.float64, 2, [(8, 45), (6, 20)], start_buffer=4, end_buffer=4,
+                       initial_window=10)
+    assert s.layout() == (16, 2)
+    assert np.any(om.kind == 2)
+
+
 def test_progress_semantics_with_mass(gm, oracle):
     t = _gauss(gm, np.diag([0.25, 2.0, 1.0]))
     x0 = gm.init_with_seed(10, 3, 6, np.float64)
