@@ -29,6 +29,67 @@ __device__ __forceinline__ float load_f32(const T* base, long long idx) {
   return (float)base[idx];
 }
 
+// Fallback for series too long for series_lag_kernel's LDS staging
+// (h beyond ~35,000 draws per split chain): the direct per-thread form.
+// blockDim.x = PT * KB: PT parameters (fastest) x KB split chains.
+// Dynamic LDS: h * blockDim.x floats (the block's series, t-major) when use_lds.
+template <class T>
+__global__ void series_kernel(const T* __restrict__ x, long long C, long long N, long long P,
+                              long long sc, long long sd, long long sp, int h, int PT, int KB,
+                              int use_lds, double* __restrict__ cm, double* __restrict__ s2,
+                              double* __restrict__ acov_part /* [G][h][P] */) {
+  extern __shared__ float lds[];
+  const int tid = threadIdx.x;
+  const int pt = tid % PT, kb = tid / PT;
+  const long long nPB = (P + PT - 1) / PT;
+  const long long p = (long long)(blockIdx.x % nPB) * PT + pt;
+  const long long g = blockIdx.x / nPB;  // chain group
+  const long long k = g * KB + kb; // split-chain index in [0, 2C)
+  const bool valid = (p < P) && (k < 2 * C);
+  const long long chain = valid ? (k < C ? k : k - C) : 0;
+  const long long t0 = (k < C) ? 0 : N - h;
+  const T* __restrict__ base = x + chain * sc + (valid ? p : 0) * sp;
+  const int nth = blockDim.x;
+  // pass 1: load to LDS (or not) and the mean
+  double sum = 0.0;
+  for (int t = 0; t < h; ++t) {
+    const float y = valid ? load_f32(base, (t0 + t) * sd) : 0.0f;
+    if (use_lds) lds[t * nth + tid] = y;
+    sum += (double)y;
+  }
+  const double mean = valid ? sum / (double)h : 0.0;
+  auto Y = [&](int t) -> double {
+    const float y = use_lds ? lds[t * nth + tid] : (valid ? load_f32(base, (t0 + t) * sd) : 0.0f);
+    return (double)y - mean;
+  };
+  double sq = 0.0;
+  for (int t = 0; t < h; ++t) {
+    const double d = Y(t);
+    sq += d * d;
+  }
+  if (valid) {
+    cm[p * 2 * C + k] = mean;
+    s2[p * 2 * C + k] = sq / (double)h;
+  }
+  __syncthreads();  // all series loaded before LDS is reused below
+  // autocovariance, summed over the KB chains of this block for each (l, p)
+  double* red = (double*)(lds + (use_lds ? (long long)h * nth : 0));
+  for (int l = 0; l < h; ++l) {
+    double acc = 0.0;
+    for (int t = 0; t + l < h; ++t) acc += Y(t) * Y(t + l);
+    acc = valid ? acc / (double)h : 0.0;
+    // reduce over kb for the same pt (fixed tree order)
+    red[tid] = acc;
+    __syncthreads();
+    for (int w = KB / 2; w >= 1; w >>= 1) {
+      if (kb < w) red[tid] = red[tid] + red[tid + w * PT];
+      __syncthreads();
+    }
+    if (kb == 0 && p < P) acov_part[(g * h + l) * P + p] = red[tid];
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // series_lag_kernel: the same products for h > 64 (long runs), one wave per
 // parameter. Block = LT_PT waves = LT_PT consecutive parameters x one chain
@@ -44,8 +105,8 @@ __device__ __forceinline__ float load_f32(const T* base, long long idx) {
 // banks, and zero-padded past h so that no lane tests bounds. The group's sums
 // stay in registers across its chains; acov_part[g][l][p] = sum / h. Lags
 // beyond 512 take further passes over the group (h > 512 only).
-constexpr int LT_PT = 8;                // parameters (waves) per block
-constexpr int LT_T = LT_PT * 64;        // threads per block
+constexpr int LT_PT = 8;                // parameters (waves) per block, at most
+constexpr int LT_T = LT_PT * 64;        // threads per block, at most
 constexpr int LT_LAGS = 512;            // lags per pass (64 lanes x 8)
 __host__ __device__ constexpr int lt_skew(int i) { return i + (i >> 3); }
 __host__ __device__ constexpr int lt_stride(int h) { return lt_skew(h + LT_LAGS + 8) + 1; }
@@ -53,12 +114,12 @@ __host__ __device__ constexpr int lt_stride(int h) { return lt_skew(h + LT_LAGS 
 template <class T>
 __global__ __launch_bounds__(LT_T) void series_lag_kernel(const T* __restrict__ x, long long C, long long N,
                                                           long long P, long long sc, long long sd, long long sp,
-                                                          int h, long long nPT, long long KPG,
+                                                          int h, int PT, long long nPT, long long KPG,
                                                           double* __restrict__ cm, double* __restrict__ s2,
                                                           double* __restrict__ acov_part /* [G][h][P] */) {
-  extern __shared__ float ys[];  // [LT_PT][stride] skewed series
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const long long pt0 = (long long)(blockIdx.x % nPT) * LT_PT;
+  extern __shared__ float ys[];  // [PT][stride] skewed series
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nt = PT * 64;
+  const long long pt0 = (long long)(blockIdx.x % nPT) * PT;
   const long long g = blockIdx.x / nPT;
   const long long p = pt0 + w;
   const bool pvalid = p < P;
@@ -76,8 +137,8 @@ __global__ __launch_bounds__(LT_T) void series_lag_kernel(const T* __restrict__ 
       const long long t0 = k < C ? 0 : N - h;
       __syncthreads();  // the previous series is no longer read
       // stage: consecutive threads take consecutive parameters of one draw
-      for (int i = tid; i < h * LT_PT; i += LT_T) {
-        const int t = i / LT_PT, q = i - t * LT_PT;
+      for (int i = tid; i < h * PT; i += nt) {
+        const int t = i / PT, q = i - t * PT;
         const long long pq = pt0 + q;
         ys[q * stride + lt_skew(t)] = pq < P ? load_f32(x + chain * sc + pq * sp, (t0 + t) * sd) : 0.0f;
       }
@@ -410,9 +471,12 @@ int diag_series(gm_dtype dt, const void* x, long long C, long long N, long long 
       hipLaunchKernelGGL(series_gram_kernel<double>, grid, dim3(GT_T), lds, st, (const double*)x,
                          C, N, P, sc, sd, sp, h, (int)nPT, CPG, cm, s2, (double*)ws.part);
     e = hipGetLastError();
-  } else {
-    // long series: ~512 blocks of LT_PT waves over chain groups of split chains
-    const long long nPT = (P + LT_PT - 1) / LT_PT;
+  } else if ((size_t)lt_stride(h) * sizeof(float) <= 150 * 1024) {
+    // long series: ~512 blocks of PT waves (PT parameters, as many as the
+    // LDS staging allows, at most LT_PT) over chain groups of split chains
+    int PT = (int)((150 * 1024) / ((size_t)lt_stride(h) * sizeof(float)));
+    if (PT > LT_PT) PT = LT_PT;
+    const long long nPT = (P + PT - 1) / PT;
     G = (512 + nPT - 1) / nPT;
     if (G > 2 * C) G = 2 * C;
     const long long KPG = (2 * C + G - 1) / G;
@@ -423,18 +487,46 @@ int diag_series(gm_dtype dt, const void* x, long long C, long long N, long long 
     }
     int rc = ensure_part((size_t)G * h * P * sizeof(double));
     if (rc) return rc;
-    const size_t lds = (size_t)LT_PT * lt_stride(h) * sizeof(float);
-    if (lds > 160 * 1024) {
-      set_error("diagnostics: series too long for the LDS staging (h > ~4500)");
-      return GM_EINVAL;
-    }
+    const size_t lds = (size_t)PT * lt_stride(h) * sizeof(float);
     dim3 grid((unsigned)(nPT * G));
     if (dt == GM_F32)
-      hipLaunchKernelGGL(series_lag_kernel<float>, grid, dim3(LT_T), lds, st, (const float*)x, C, N, P, sc,
-                         sd, sp, h, nPT, KPG, cm, s2, (double*)ws.part);
+      hipLaunchKernelGGL(series_lag_kernel<float>, grid, dim3(PT * 64), lds, st, (const float*)x, C, N, P, sc,
+                         sd, sp, h, PT, nPT, KPG, cm, s2, (double*)ws.part);
     else
-      hipLaunchKernelGGL(series_lag_kernel<double>, grid, dim3(LT_T), lds, st, (const double*)x, C, N, P,
-                         sc, sd, sp, h, nPT, KPG, cm, s2, (double*)ws.part);
+      hipLaunchKernelGGL(series_lag_kernel<double>, grid, dim3(PT * 64), lds, st, (const double*)x, C, N, P,
+                         sc, sd, sp, h, PT, nPT, KPG, cm, s2, (double*)ws.part);
+    e = hipGetLastError();
+  } else {  // very long series: the direct per-thread kernel
+    int PT = 1;
+    while (PT < P && PT < 16) PT <<= 1;
+    int nth;
+    int use_lds = 1;
+    if ((long long)h * 256 * 4 + 256 * 8 <= 150 * 1024) nth = 256;
+    else if ((long long)h * 128 * 4 + 128 * 8 <= 150 * 1024) nth = 128;
+    else if ((long long)h * 64 * 4 + 64 * 8 <= 150 * 1024) nth = 64;
+    else {
+      nth = 256;
+      use_lds = 0;
+    }
+    if (nth < PT) nth = PT;
+    const int KB = nth / PT;
+    G = (2 * C + KB - 1) / KB;
+    int rc = ensure_part((size_t)G * h * P * sizeof(double));
+    if (rc) return rc;
+    const size_t lds = (use_lds ? (size_t)h * nth * 4 : 0) + (size_t)nth * 8;
+    const long long nblk = ((P + PT - 1) / PT) * G;
+    if (nblk > 0x7fffffffLL) {
+      set_error("diagnostics: problem too large for one launch");
+      return GM_EINVAL;
+    }
+    dim3 grid((unsigned)nblk);
+    if (dt == GM_F32)
+      hipLaunchKernelGGL(series_kernel<float>, grid, dim3(nth), lds, st, (const float*)x, C, N, P, sc,
+                         sd, sp, h, PT, KB, use_lds, cm, s2, (double*)ws.part);
+    else
+      hipLaunchKernelGGL(series_kernel<double>, grid, dim3(nth), lds, st, (const double*)x, C, N, P,
+                         sc, sd, sp, h, PT, KB, use_lds, cm, s2, (double*)ws.part);
+
     e = hipGetLastError();
   }
   if (e != hipSuccess) {

@@ -146,10 +146,11 @@ def test_nuts_chain_1_kat(gm):
 
 # h = N/2 <= 64 runs the matrix-core Gram kernel (chain groups, 8-parameter
 # tiles: C and P chosen off those multiples), larger h the register-window lag
-# kernel (8-parameter blocks; h > 512 takes a second pass over the lags)
+# kernel (up to 8-parameter blocks, fewer when a long series fills the LDS;
+# h > 512 takes further passes over the lags)
 @pytest.mark.parametrize("shape", [(4, 100, 3), (7, 41, 2), (64, 300, 5), (3, 1000, 1),
                                    (100, 128, 37), (33, 129, 17), (517, 60, 9), (9, 131, 3),
-                                   (5, 1100, 3), (20, 200, 19)])
+                                   (5, 1100, 3), (20, 200, 19), (3, 8000, 2), (2, 10400, 1)])
 @pytest.mark.parametrize("dtype", DTYPES)
 def test_split_rhat_ess_matches_oracle(gm, oracle, shape, dtype):
     rng = np.random.default_rng(sum(shape))
