@@ -487,6 +487,9 @@ extern __shared__ __attribute__((aligned(16))) unsigned char gm_dyn_lds[];
 #ifndef GM_GEMV_UNROLL
 #define GM_GEMV_UNROLL 4  // columns of the LDS GEMV loop in flight per iteration
 #endif
+// matrix-core form: a chain's d / w slot in LDS, 32 doubles padded to 34 so
+// that the 4 chains of a wave fall in different banks (16-byte aligned)
+#define GM_MF_SLOT 34
 template <class T, int LPC, int E> struct GaussLane;
 template <class T> struct GaussT {
   const T* mu;    // [D] device
@@ -500,7 +503,7 @@ template <class T> struct GaussT {
   }
   // dynamic LDS bytes a 256-thread block needs for layout (LPC, E)
   template <int LPC, int E> __host__ __device__ static size_t lds_need(int D) {
-    if (mfma_form<LPC, E>() && D <= 32) return ((size_t)1024 + (size_t)2 * 256 * E) * sizeof(T);
+    if (mfma_form<LPC, E>() && D <= 32) return ((size_t)1024 + (size_t)2 * (256 / LPC) * GM_MF_SLOT) * sizeof(T);
     return ((size_t)D * LPC * E + (size_t)256 * E) * sizeof(T);
   }
   template <int LPC, int E> __host__ __device__ size_t lds_bytes() const {
@@ -527,7 +530,7 @@ template <class T> struct GaussT {
         }
         __syncthreads();
         r.sprec = sp;
-        r.sd = sp + 1024 + (threadIdx.x >> 4) * 32;
+        r.sd = sp + 1024 + (threadIdx.x >> 4) * GM_MF_SLOT;
         r.mf = true;
         return r;
       }
@@ -594,7 +597,7 @@ template <class T, int LPC, int E> struct GaussLane {
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       // B: chain l&3's d_{4s + (l>>4)}, s = 0..7
-      const T* bt = sprec + 1024 + (wb + (l & 3)) * 32 + (l >> 4) * 8;
+      const T* bt = sprec + 1024 + (wb + (l & 3)) * GM_MF_SLOT + (l >> 4) * 8;
       v2 bv[4], av[8];
 #pragma unroll
       for (int t = 0; t < 4; ++t) bv[t] = *(const v2*)(bt + 2 * t);
@@ -608,14 +611,14 @@ template <class T, int LPC, int E> struct GaussLane {
         acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(av[4 + (s >> 1)][s & 1], b, acc1, 0, 0, 0);
       }
       // D[m = l>>4][n = l&3] of block (l>>2)&3: chain l&3's w at row 4((l>>2)&3) + (l>>4) (+16)
-      T* ws = const_cast<T*>(sprec) + 1536;
+      T* ws = const_cast<T*>(sprec) + 1024 + 16 * GM_MF_SLOT;  // after the 16 d slots of the block
       const int row = 4 * ((l >> 2) & 3) + (l >> 4);
-      ws[(wb + (l & 3)) * 32 + row] = acc0;
-      ws[(wb + (l & 3)) * 32 + 16 + row] = acc1;
+      ws[(wb + (l & 3)) * GM_MF_SLOT + row] = acc0;
+      ws[(wb + (l & 3)) * GM_MF_SLOT + 16 + row] = acc1;
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const v2 wv = *(const v2*)(ws + (threadIdx.x >> 4) * 32 + (l & 15) * E);
+      const v2 wv = *(const v2*)(ws + (threadIdx.x >> 4) * GM_MF_SLOT + (l & 15) * E);
       w[0] = wv[0];
       w[1] = wv[1];
 #ifdef GM_NUTS_PROF
