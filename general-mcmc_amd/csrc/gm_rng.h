@@ -260,17 +260,25 @@ GM_HD double gexp(double x) {
   const double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
                P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
                P5 = 4.13813679705723846039e-08;
-  if (x != x) return x;
-  if (x > o_th) return u2d(0x7ff0000000000000ull);
-  if (x < u_th) return 0.0;
-  const int k = (int)(invln2 * x + (x < 0.0 ? -0.5 : 0.5));
+  // Branch-free (the NUTS leaf evaluates it for every chain of a wave): the
+  // main path runs on a safe input and the special cases are selected at
+  // the end; scale2's three forms are selected by their exponent fields.
+  // Same values as the branching form.
+  const bool nan = x != x, over = x > o_th, under = x < u_th;
+  const double xs = (nan || over || under) ? 0.0 : x;
+  const int k = (int)(invln2 * xs + (xs < 0.0 ? -0.5 : 0.5));
   const double dk = (double)k;
-  const double hi = x - dk * ln2HI, lo = dk * ln2LO;
+  const double hi = xs - dk * ln2HI, lo = dk * ln2LO;
   const double r = hi - lo;
   const double t = r * r;
   const double c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
   const double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
-  return scale2(y, k);
+  // scale2(y, k): (y * 2^1023) * 2^(k-1023) | (y * 2^(k+1000)) * 2^-1000 | (y * 2^k) * 1
+  const bool big = k > 1023, small = k < -1021;
+  const int e1 = big ? 2046 : small ? k + 2023 : k + 1023;
+  const int e2 = big ? k : small ? 23 : 1023;
+  const double res = (y * u2d((uint64_t)(uint32_t)e1 << 52)) * u2d((uint64_t)(uint32_t)e2 << 52);
+  return nan ? x : over ? u2d(0x7ff0000000000000ull) : under ? 0.0 : res;
 }
 GM_HD float scale2f(float y, int k) {
   if (k > 127) return y * u2f(0x7f000000u) * u2f((uint32_t)(k - 127 + 127) << 23);
