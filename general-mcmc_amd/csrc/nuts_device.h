@@ -662,9 +662,28 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       stack_scalars(k, lal, ln_, lna);
       const double u = nuts_u<double>(key, 64u + merge_ctr++);
       const int den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
-      if (!(u < (double)tn / (double)den)) stack_vec(k, 2, pr);
+      // (selects rather than branches from here on: the chains of a wave
+      // take different sides, and a divergent branch costs both)
+      {
+        const bool keep_left = !(u < (double)tn / (double)den);
+        T lpr[E];
+        stack_vec(k, 2, lpr);
+#pragma unroll
+        for (int e = 0; e < E; ++e) pr[e] = keep_left ? lpr[e] : pr[e];
+      }
       tn = ln_ + tn;
-      if (ts) ts = (v > 0) ? no_uturn<LPC, E>(lq, qe, lpv, pe) : no_uturn<LPC, E>(qe, lq, pe, lpv);
+      {
+        T qm[E], qp[E], pm[E], pp[E];  // U-turn over the merged subtree's ends, minus side first
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          qm[e] = v > 0 ? lq[e] : qe[e];
+          qp[e] = v > 0 ? qe[e] : lq[e];
+          pm[e] = v > 0 ? lpv[e] : pe[e];
+          pp[e] = v > 0 ? pe[e] : lpv[e];
+        }
+        const bool nu = no_uturn<LPC, E>(qm, qp, pm, pp);
+        ts = ts && nu;
+      }
       ta = lal + ta;
       tna = lna + tna;
 #pragma unroll
@@ -686,14 +705,13 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     {
       const T tmp = rust_min1((T)tn / (T)n);
       const T u2 = nuts_u<T>(key, 2u * (uint32_t)j + 1u);
-      if (ts && (u2 < tmp)) {
+      const bool move = ts && (u2 < tmp);
 #pragma unroll
-        for (int e = 0; e < E; ++e) q[e] = pr[e];
-        ++acc;
-      }
+      for (int e = 0; e < E; ++e) q[e] = move ? pr[e] : q[e];
+      acc += move ? 1 : 0;
       n += tn;
       bool s_ok = ts;
-      if (s_ok) {
+      {
         T qmv[E], qpv[E], pmv[E], ppv[E];
 #pragma unroll
         for (int e = 0; e < E; ++e) {
@@ -702,19 +720,26 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
           pmv[e] = v > 0 ? pf[e] : pe[e];
           ppv[e] = v > 0 ? pe[e] : pf[e];
         }
-        s_ok = no_uturn_m<LPC, E>(M, qmv, qpv, pmv, ppv, lane);
+        if constexpr (MASS == 2) {  // the dense products: only where needed
+          if (s_ok) s_ok = no_uturn_m<LPC, E>(M, qmv, qpv, pmv, ppv, lane);
+        } else {
+          const bool nu = no_uturn_m<LPC, E>(M, qmv, qpv, pmv, ppv, lane);
+          s_ok = s_ok && nu;
+        }
       }
       ++j;
       if (s_ok && j < a.max_depth) {  // next doubling
         const int v2 = (nuts_u<T>(key, 2u * (uint32_t)j) < (T)0.5) ? 1 : -1;
-        if (v2 != v) {  // integrate from the other end
+        const bool sw = v2 != v;  // integrate from the other end
 #pragma unroll
-          for (int e = 0; e < E; ++e) {
-            T t;
-            t = qe[e]; qe[e] = qf[e]; qf[e] = t;
-            t = pe[e]; pe[e] = pf[e]; pf[e] = t;
-            t = ge[e]; ge[e] = gf[e]; gf[e] = t;
-          }
+        for (int e = 0; e < E; ++e) {
+          const T a0 = qe[e], a1 = pe[e], a2 = ge[e];
+          qe[e] = sw ? qf[e] : qe[e];
+          pe[e] = sw ? pf[e] : pe[e];
+          ge[e] = sw ? gf[e] : ge[e];
+          qf[e] = sw ? a0 : qf[e];
+          pf[e] = sw ? a1 : pf[e];
+          gf[e] = sw ? a2 : gf[e];
         }
         v = v2;
         l = 0;
