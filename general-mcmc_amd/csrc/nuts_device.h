@@ -262,9 +262,8 @@ __device__ __forceinline__ bool group_all_finite(const T (&x)[E], int lane, int 
   return group_sum<LPC>(bad) == 0;
 }
 
-template <class T> __device__ __forceinline__ T rust_min1(T x) {  // T::one().min(x)
-  if (x != x) return (T)1;
-  return x < (T)1 ? x : (T)1;
+template <class T> __device__ __forceinline__ T rust_min1(T x) {  // T::one().min(x): NaN -> 1
+  return (x != x) ? (T)1 : (x < (T)1 ? x : (T)1);
 }
 
 template <class T> struct MachEps;
@@ -573,7 +572,16 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       }
       momentum_from<LPC, E>(M, z, p0, lane);
     }
-    if (live && !starting) {  // leapfrog_with_mass (:1396-1418): kick, drift by M^-1 p
+    if constexpr (MASS == 0) {  // leapfrog (:1396-1418), as selects: kick, drift
+      const bool adv = live && !starting;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const T pk = pe[e] + ge[e] * h;
+        const T qk = qe[e] + pk * epsv;
+        pe[e] = adv ? pk : pe[e];
+        qe[e] = adv ? qk : qe[e];
+      }
+    } else if (live && !starting) {  // leapfrog_with_mass (:1396-1418): kick, drift by M^-1 p
 #pragma unroll
       for (int e = 0; e < E; ++e) pe[e] = pe[e] + ge[e] * h;
       T vv[E];
@@ -585,9 +593,13 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     for (int e = 0; e < E; ++e) x[e] = starting ? q[e] : qe[e];
     T sums[2];
     sums[0] = tg.template eval_part<LPC, E>(x, gx, lane);
-    if (live && !starting) {
+    {
+      const bool adv = live && !starting;
 #pragma unroll
-      for (int e = 0; e < E; ++e) pe[e] = pe[e] + gx[e] * h;
+      for (int e = 0; e < E; ++e) {
+        const T pk = pe[e] + gx[e] * h;
+        pe[e] = adv ? pk : pe[e];
+      }
     }
     {
       T pk[E];
