@@ -253,13 +253,29 @@ GM_HD double scale2(double y, int k) {  // y * 2^k, y in [0.5, 2]
   if (k < -1021) return y * u2d((uint64_t)(k + 1000 + 1023) << 52) * u2d((uint64_t)(-1000 + 1023) << 52);
   return y * u2d((uint64_t)(k + 1023) << 52);
 }
-GM_HD double gexp(double x) {
-  const double o_th = 7.09782712893383973096e+02, u_th = -7.45133219101941108420e+02;
-  const double ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10;
-  const double invln2 = 1.44269504088896338700e+00;
-  const double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
-               P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
-               P5 = 4.13813679705723846039e-08;
+// The constants of gexp(double); ExpConsts::pinned() holds them in VGPRs for a
+// hot loop (a VALU operation with an SGPR operand issues at about half rate,
+// and the compiler otherwise rebuilds each 64-bit constant with two scalar
+// moves at every use). Same values either way.
+struct ExpConsts {
+  double o_th = 7.09782712893383973096e+02, u_th = -7.45133219101941108420e+02;
+  double ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10;
+  double invln2 = 1.44269504088896338700e+00;
+  double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+         P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+         P5 = 4.13813679705723846039e-08;
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+  __device__ static ExpConsts pinned() {
+    ExpConsts K;
+    asm volatile("" : "+v"(K.o_th), "+v"(K.u_th), "+v"(K.ln2HI), "+v"(K.ln2LO), "+v"(K.invln2));
+    asm volatile("" : "+v"(K.P1), "+v"(K.P2), "+v"(K.P3), "+v"(K.P4), "+v"(K.P5));
+    return K;
+  }
+#endif
+};
+GM_HD double gexp(double x, const ExpConsts& K) {
+  const double o_th = K.o_th, u_th = K.u_th, ln2HI = K.ln2HI, ln2LO = K.ln2LO, invln2 = K.invln2;
+  const double P1 = K.P1, P2 = K.P2, P3 = K.P3, P4 = K.P4, P5 = K.P5;
   // Branch-free (the NUTS leaf evaluates it for every chain of a wave): the
   // main path runs on a safe input and the special cases are selected at
   // the end; scale2's three forms are selected by their exponent fields.
@@ -280,6 +296,7 @@ GM_HD double gexp(double x) {
   const double res = (y * u2d((uint64_t)(uint32_t)e1 << 52)) * u2d((uint64_t)(uint32_t)e2 << 52);
   return nan ? x : over ? u2d(0x7ff0000000000000ull) : under ? 0.0 : res;
 }
+GM_HD double gexp(double x) { return gexp(x, ExpConsts{}); }
 GM_HD float scale2f(float y, int k) {
   if (k > 127) return y * u2f(0x7f000000u) * u2f((uint32_t)(k - 127 + 127) << 23);
   if (k < -125) return y * u2f((uint32_t)(k + 100 + 127) << 23) * u2f((uint32_t)(-100 + 127) << 23);
@@ -301,6 +318,7 @@ GM_HD float gexp(float x) {
   const float y = 1.0f - ((lo - (r * c) / (2.0f - c)) - hi);
   return scale2f(y, k);
 }
+GM_HD float gexp(float x, const ExpConsts&) { return gexp(x); }
 
 // ---- cos / sin of 2*pi*u, u in [0,1) ---------------------------------------
 // Quadrant q = floor(4u), r = u - q/4 in [0, 1/4) (both exact); the first

@@ -538,6 +538,10 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   // pending at the loop entry, the wait the compiler puts at the loop head
   // would also wait out the previous transition's sample stores.
   __builtin_amdgcn_s_waitcnt(0);
+  const ExpConsts ek = [] {  // the leaf's f64 exp, constants in VGPRs
+    if constexpr (sizeof(T) == 8) return ExpConsts::pinned();
+    else return ExpConsts{};
+  }();
   while (true) {
     const bool live = s < a.n_steps;
 #ifdef GM_NUTS_PROF
@@ -645,7 +649,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     const T joint = lp - kin;
     tn = (logu < joint) ? 1 : 0;
     ts = (logu - (T)1000) < joint;
-    ta = rust_min1(gexp(joint - joint0));
+    ta = rust_min1(gexp(joint - joint0, ek));
     tna = 1;
 #pragma unroll
     for (int e = 0; e < E; ++e) { fq[e] = qe[e]; fp[e] = pe[e]; pr[e] = qe[e]; }
