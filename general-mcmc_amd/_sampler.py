@@ -197,6 +197,8 @@ class Sampler:
     def reserve(self, n_collect: int):
         """Pre-size the device sample buffer for runs of up to n_collect
         collected transitions (no allocation inside those runs)."""
+        # growing the buffer frees the one earlier DeviceSamples point into
+        self._gen += 1
         _lib.check(self._lib.gm_sampler_reserve(self._h, n_collect))
         return self
 

@@ -310,8 +310,10 @@ int gm_device_count(int* count) {
 // 4 us less wall time on the bench's first timed run
 // (profiles/r02/launch_ab.json).
 int gm_set_device(int device) {
-  hipSetDeviceFlags(hipDeviceScheduleSpin);  // ignored once the device is initialised
   GM_HIP(hipSetDevice(device));
+  // after hipSetDevice, so that the flag applies to `device` (ignored once
+  // that device is initialised)
+  hipSetDeviceFlags(hipDeviceScheduleSpin);
   return GM_OK;
 }
 
@@ -608,13 +610,14 @@ static int hmc_lf_unroll(long long waves) {
 }
 
 // hipSetDevice only when the calling thread is on another device (the call
-// is on every run's path)
+// is on every run's path). The current device is asked of the runtime
+// (a thread-local read in HIP), never cached here: gm_set_device and the
+// other entry points switch devices too.
 static hipError_t use_device(int dev) {
-  static thread_local int cur = -1;
-  if (cur == dev) return hipSuccess;
-  const hipError_t e = hipSetDevice(dev);
-  if (e == hipSuccess) cur = dev;
-  return e;
+  int cur = -1;
+  const hipError_t g = hipGetDevice(&cur);
+  if (g == hipSuccess && cur == dev) return hipSuccess;
+  return hipSetDevice(dev);
 }
 
 // One event pair per run (before the first launch, after the last): the

@@ -1,6 +1,7 @@
 // gmcmc_bv.cpp — C ABI of the granular BatchVector ops (tier 2 of the
 // boundary, include/gmcmc.h): argument checks, then one kernel launch each
 // (bv_kernels.hip) on the null stream.
+#include <map>
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -96,7 +97,15 @@ int gm_bv_fill(gm_dtype dt, int64_t n, void* x, double value) {
 }
 int gm_bv_dot(gm_dtype dt, int64_t n, const void* a, const void* b, double* out) {
   BV_REQ(dtype_ok(dt) && n >= 0 && out && ((a && b) || n == 0), "bad arguments");
-  static thread_local double* dres = nullptr;
+  // one result slot per device (the calling thread may switch devices
+  // between calls; a slot is never used across devices)
+  static thread_local std::map<int, double*> slots;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    set_error("hipGetDevice failed in dot");
+    return GM_EHIP;
+  }
+  double*& dres = slots[dev];
   if (!dres && hipMalloc(&dres, sizeof(double)) != hipSuccess) {
     dres = nullptr;
     set_error("device allocation failed in dot");

@@ -81,8 +81,6 @@ struct gm_comm {
   int rank = 0;
   int device = 0;
   hipStream_t stream = nullptr;
-  // shapes (C, N, P, dtype) already checked equal on every rank
-  std::set<std::array<long long, 4>> checked;
 };
 
 static int local_diag(const void* dev_sample, gm_dtype dtype, int64_t C, int64_t N, int64_t P,
@@ -108,12 +106,13 @@ static int local_diag(const void* dev_sample, gm_dtype dtype, int64_t C, int64_t
   const double *pcm = (double*)cm.p, *ps2 = (double*)s2.p, *pac = (double*)ac.p;
   if (R > 1) {
     // Every rank must pass the same shape: the grouped all-gather below is
-    // sized from it, and unequal sizes would not match up across ranks. A
-    // shape is checked once per communicator (one 4-word all-gather + host
-    // sync), then trusted: the ranks call in lockstep with equal shapes, so
-    // they all take the same branch here.
-    const std::array<long long, 4> shape{(long long)C, (long long)N, (long long)P, (long long)dtype};
-    if (!comm->checked.count(shape)) {
+    // sized from it, and unequal sizes would not match up across ranks (a
+    // hang or corrupt data). The shape is therefore checked on EVERY call
+    // (one 4-word all-gather + a host sync, tens of microseconds against the
+    // summaries' kernels): a mismatch is GM_EINVAL on every rank, never a
+    // mismatched collective.
+    {
+      const std::array<long long, 4> shape{(long long)C, (long long)N, (long long)P, (long long)dtype};
       DevBuf &cnt = B.cnt, &cnt_all = B.cnt_all;
       if ((rc = cnt.alloc(sizeof(shape))) || (rc = cnt_all.alloc(sizeof(shape) * R))) return rc;
       GM_HIP(hipMemcpyAsync(cnt.p, shape.data(), sizeof(shape), hipMemcpyHostToDevice, st));
@@ -126,7 +125,6 @@ static int local_diag(const void* dev_sample, gm_dtype dtype, int64_t C, int64_t
           set_error("gm_split_rhat_ess_dist: all ranks must pass the same chain count, draws, params and dtype");
           return GM_EINVAL;
         }
-      comm->checked.insert(shape);
     }
     if ((rc = cm_all.alloc(sizeof(double) * 2 * C * P * R)) ||
         (rc = s2_all.alloc(sizeof(double) * 2 * C * P * R)) ||

@@ -494,16 +494,22 @@ void or_autocov_fft(const float* x, int64_t n, int64_t d, float* out) {
   free(im);
 }
 
-/* split_rhat_mean_ess (stats.rs:439-573) on an f32 [C][N][P] sample. */
-void or_split_rhat_ess(const float* x, int64_t C, int64_t N, int64_t P, float* rhat, float* ess) {
+/* split_rhat_mean_ess (stats.rs:439-573) on parameters [p0, p0 + P) of an
+ * f32 [C][N][Ptot] sample; rhat/ess receive P values. Parameters are
+ * independent in every step of the reference (withinvar and ess map over
+ * them, stats.rs:463-466, 545-548; the chain-axis mean of ess is
+ * elementwise, :535), so a parameter range computes the same bits as the
+ * whole sample does for those parameters. */
+static void split_rhat_ess_range(const float* x, int64_t C, int64_t N, int64_t Ptot, int64_t p0,
+                                 int64_t P, float* rhat, float* ess) {
   const int64_t h = N / 2, K = 2 * C;
   /* splitcat: [2C][h][P] */
   float* y = (float*)malloc(sizeof(float) * (size_t)(K * h * P > 0 ? K * h * P : 1));
   for (int64_t c = 0; c < C; ++c)
     for (int64_t t = 0; t < h; ++t)
       for (int64_t p = 0; p < P; ++p) {
-        y[(c * h + t) * P + p] = x[(c * N + t) * P + p];
-        y[((C + c) * h + t) * P + p] = x[(c * N + (N - h) + t) * P + p];
+        y[(c * h + t) * P + p] = x[(c * N + t) * Ptot + p0 + p];
+        y[((C + c) * h + t) * P + p] = x[(c * N + (N - h) + t) * Ptot + p0 + p];
       }
   float* within = (float*)malloc(sizeof(float) * P);
   float* var = (float*)malloc(sizeof(float) * P);
@@ -554,6 +560,41 @@ void or_split_rhat_ess(const float* x, int64_t C, int64_t N, int64_t P, float* r
     ess[p] = (1.0f / tau) * (float)K * (float)h;
   }
   free(y); free(within); free(var); free(cms); free(sq); free(avg); free(ac);
+}
+
+void or_split_rhat_ess(const float* x, int64_t C, int64_t N, int64_t P, float* rhat, float* ess) {
+  split_rhat_ess_range(x, C, N, P, 0, P, rhat, ess);
+}
+
+/* The same on `nthreads` threads, each owning a contiguous parameter range
+ * (the reference's rayon map over parameters, stats.rs:464, 546); results
+ * are bitwise those of or_split_rhat_ess. Lets the config-size parity tests
+ * (65,536-262,144 split chains) finish in seconds. */
+typedef struct {
+  const float* x;
+  int64_t C, N, P, p0, np;
+  float *rhat, *ess;
+} srange_job;
+static void* srange_worker(void* arg) {
+  srange_job* j = (srange_job*)arg;
+  if (j->np > 0) split_rhat_ess_range(j->x, j->C, j->N, j->P, j->p0, j->np, j->rhat + j->p0, j->ess + j->p0);
+  return NULL;
+}
+void or_split_rhat_ess_mt(const float* x, int64_t C, int64_t N, int64_t P, float* rhat, float* ess,
+                          int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > P) nthreads = (int)P;
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  srange_job* jobs = (srange_job*)malloc(sizeof(srange_job) * (size_t)nthreads);
+  for (int i = 0; i < nthreads; ++i) {
+    const int64_t a = P * i / nthreads, b = P * (i + 1) / nthreads;
+    srange_job j = {x, C, N, P, a, b - a, rhat, ess};
+    jobs[i] = j;
+    pthread_create(&th[i], NULL, srange_worker, &jobs[i]);
+  }
+  for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+  free(th);
+  free(jobs);
 }
 
 /* MultiChainTracker (stats.rs:199-339): step() updates, then rhat(). */

@@ -161,6 +161,8 @@ void or_build_tree_d(const or_target* t, int lanes, int elems, const double* q, 
 
 /* ---- diagnostics: stats.rs (f32, the reference's arithmetic) ---- */
 void or_split_rhat_ess(const float* x, int64_t C, int64_t N, int64_t P, float* rhat, float* ess);
+void or_split_rhat_ess_mt(const float* x, int64_t C, int64_t N, int64_t P, float* rhat, float* ess,
+                          int nthreads);
 void or_autocov_bf(const float* x, int64_t n, int64_t d, float* out);
 void or_autocov_fft(const float* x, int64_t n, int64_t d, float* out);
 /* MultiChainTracker: steps [nsteps][C][P] -> rhat [P] (stats.rs:199-339) */

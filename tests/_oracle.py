@@ -76,6 +76,7 @@ def load():
     lib.or_build_tree_d.argtypes = [tp, _int, _int, _vp, _vp, _vp, _dbl, _int, _int, _dbl, _dbl,
                                     _u64, _u32, _u64, _vp, _vp]
     lib.or_split_rhat_ess.argtypes = [_vp, _i64, _i64, _i64, _vp, _vp]
+    lib.or_split_rhat_ess_mt.argtypes = [_vp, _i64, _i64, _i64, _vp, _vp, C.c_int]
     lib.or_autocov_bf.argtypes = [_vp, _i64, _i64, _vp]
     lib.or_autocov_fft.argtypes = [_vp, _i64, _i64, _vp]
     lib.or_mct_rhat.argtypes = [_vp, _i64, _i64, _i64, _vp]
@@ -267,12 +268,18 @@ class Oracle:
         assert rc == 0
         return q, acc, nlf
 
-    def split_rhat_ess(self, x):
+    def split_rhat_ess(self, x, threads: int = 1):
+        """split_rhat_mean_ess (stats.rs:439-450) of a [C, N, P] sample (cast
+        to f32 first, stats.rs:443); threads > 1 splits the parameters over
+        threads (bitwise the same result)."""
         x = np.ascontiguousarray(x, dtype=np.float32)
         c, n, p = x.shape
         r = np.empty(p, dtype=np.float32)
         e = np.empty(p, dtype=np.float32)
-        self.lib.or_split_rhat_ess(_p(x), c, n, p, _p(r), _p(e))
+        if threads > 1:
+            self.lib.or_split_rhat_ess_mt(_p(x), c, n, p, _p(r), _p(e), int(threads))
+        else:
+            self.lib.or_split_rhat_ess(_p(x), c, n, p, _p(r), _p(e))
         return r, e
 
     def autocov(self, x, fft=False):

@@ -89,3 +89,30 @@ def test_copy_samples_size_and_stale_device_samples(gm):
     with pytest.raises(RuntimeError):
         ds.block(0, 1, 0, 1)
     s.close()
+
+
+def test_samplers_on_two_devices_one_thread(gm):
+    """One thread drives samplers on two devices with gm_set_device calls in
+    between: every run must use its own sampler's device (the library asks
+    the runtime for the current device instead of caching it)."""
+    import ctypes as C
+    lib = gm._lib.load()
+    n = C.c_int()
+    gm._lib.check(lib.gm_device_count(C.byref(n)))
+    if n.value < 2:
+        pytest.skip("needs two GPUs")
+    x0 = gm.init_det(64, 8, np.float32)
+    gm._lib.check(lib.gm_set_device(0))
+    a = gm.HMC(gm.RosenbrockND(), x0, 0.05, 4).set_seed(1)
+    gm._lib.check(lib.gm_set_device(1))
+    b = gm.HMC(gm.RosenbrockND(), x0, 0.05, 4).set_seed(1)
+    gm._lib.check(lib.gm_set_device(0))
+    ra = a.run(5, 1)
+    gm._lib.check(lib.gm_set_device(1))
+    ra2 = a.run(3, 0)   # a's device is 0 while 1 is current
+    gm._lib.check(lib.gm_set_device(0))
+    rb = b.run(5, 1)    # b's device is 1 while 0 is current
+    np.testing.assert_array_equal(ra, rb)
+    assert ra2.shape == (64, 3, 8) and np.all(np.isfinite(ra2))
+    a.close()
+    b.close()

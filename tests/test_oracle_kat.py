@@ -110,3 +110,17 @@ def test_ess_iid_uniform(oracle):
     r, e = oracle.split_rhat_ess(u)
     assert e.min() > k["expected"]["ess_min_gt"]
     assert r.max() < k["expected"]["rhat_max_lt"]
+
+
+def test_split_rhat_ess_threads_bitwise(oracle):
+    """or_split_rhat_ess_mt (the config-size parity tests' oracle) splits the
+    parameters over threads; parameters are independent in stats.rs:456-573,
+    so the result is bitwise the single-thread restatement's."""
+    rng = np.random.default_rng(11)
+    x = (np.cumsum(rng.standard_normal((37, 120, 13)), axis=1) * 0.1
+         + rng.standard_normal((37, 120, 13))).astype(np.float32)
+    r1, e1 = oracle.split_rhat_ess(x)
+    for t in (2, 5, 13, 40):
+        rt, et = oracle.split_rhat_ess(x, threads=t)
+        np.testing.assert_array_equal(rt, r1)
+        np.testing.assert_array_equal(et, e1)

@@ -23,6 +23,10 @@ for step in "$@"; do
     fixed2) run hmc_fixed2 120 python tools/probe_hmc_fixed2.py ;;
     abhmc) run ab_hmc100 300 python tools/ab_run.py general-mcmc_amd/lib/libgmcmc.so $AB_LIBS &&
            AB_ARGS="--layouts 64x1 --rounds 3 --steps 20" run ab_hmc20 300 python tools/ab_run.py general-mcmc_amd/lib/libgmcmc.so $AB_LIBS ;;
+    diag) run diag_fullsize 600 python -u tools/diag_fullsize.py gpurun_out/diag_fullsize.jsonl ;;
+    diagtest) run diag_tests 600 python -u -m pytest tests/test_gpu_diag_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
+    abmh) AB_ROUNDS=${AB_ROUNDS:-3} run ab_mh 600 python tools/ab_mh.py ${AB_LIBS} ;;
+    abnuts) AB_ROUNDS=${AB_ROUNDS:-3} run ab_nuts 900 python tools/ab_nuts.py ${AB_LIBS} ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) run bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench) run bench 300 python bench.py ;;
