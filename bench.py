@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 VALU_F32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md, spec)
+VALU_F64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (MI355X_MICROARCH.md, spec)
 METRIC = "leapfrog steps/sec (whole node) + ESS/sec, 64-dim Rosenbrock HMC at 1/2/4/8 GPUs"
 PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_hmc.json")
 
@@ -57,10 +58,43 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="target CPU time of each CPU-baseline sample (0 disables)")
     p.add_argument("--cpu-threads", type=int, default=0, help="0: every core available to this process")
-    p.add_argument("--north-star", action="store_true",
-                   help="also time BASELINE.json north_star's 16384-chain shape (off by default, so that "
-                        "every hmc_kernel launch of the default run has the bench's shape)")
+    p.add_argument("--device-warmup-ms", type=float, default=50.0,
+                   help="untimed scratch launches of the timed shape for this long before the W warm-up "
+                        "transitions: the GPU clock ramps to its peak within ~10-30 ms of load "
+                        "(tools/probe_warmup.py, profiles/r03/warmup_probe.json)")
+    p.add_argument("--no-north-star", dest="north_star", action="store_false",
+                   help="skip the north_star 16384-chain shape (timed by default after the bench line's "
+                        "measurements)")
+    p.add_argument("--configs", default="cfg3,cfg4,cfg5",
+                   help="BASELINE.json config legs timed after the headline (comma list, '' for none)")
     return p.parse_args(argv)
+
+
+def dense_gauss_32():
+    """configs[2]'s target: mean 0, Sigma = Q diag(logspace(-1, 1,
+    32)) Q^T with Q from the QR of a seed-42 N(0,1) 32x32 matrix."""
+    rng = np.random.default_rng(42)
+    q, _ = np.linalg.qr(rng.standard_normal((32, 32)))
+    cov = q @ np.diag(np.logspace(-1, 1, 32)) @ q.T
+    return np.zeros(32), 0.5 * (cov + cov.T)
+
+
+# The BASELINE.json configs other than the headline, each a leg of its own
+# (per-GPU share; chains sharded over the ranks like the headline, R-hat/ESS
+# over every rank's chains through the RCCL all-gather when N > 1).
+CONFIG_LEGS = {
+    # configs[2]: NUTS, DenseGaussian 32-D f64, 8192 chains per GPU; NUTS::run
+    # (nuts.rs:214-259) of 500 collected after 500 warm-up transitions
+    "cfg3": dict(kind="nuts", chains=8192, dim=32, dtype="f64", n_discard=500, n_collect=500,
+                 target_accept=0.8, max_depth=10),
+    # configs[3]: batched HMC, RosenbrockND 128-D f32, 65,536 chains over 8 GPUs
+    "cfg4": dict(kind="hmc", chains=8192, dim=128, dtype="f32", n_discard=100, n_collect=100,
+                 eps=0.01, L=50),
+    # configs[4]: MH IsotropicGaussian(1) 256-D f64, proposal sd 2.38/16,
+    # 131,072 chains over 8 GPUs
+    "cfg5": dict(kind="mh", chains=16384, dim=256, dtype="f64", n_discard=1000, n_collect=100,
+                 proposal_std=2.38 / 16),
+}
 
 
 def f_alg_rosenbrock(D):
@@ -90,7 +124,48 @@ class GpuBench:
         self.dtype = np.float32 if a.dtype == "f32" else np.float64
 
     def init_positions(self, n, offset, count):
-        return self.gm.init_with_seed(n, self.a.dim, 42, np.float64)[offset:offset + count].astype(self.dtype)
+        return self.gm.init_with_seed(count, self.a.dim, 42, np.float64, row0=offset).astype(self.dtype)
+
+    def config_leg(self, name, cfg, offset, comm):
+        """One BASELINE config on this rank's share: the run timed between
+        device synchronizes (warm-up transitions included, as the reference's
+        run(n_collect, n_discard)), the kernels' HIP-event time, the work
+        counted on the device, then the device diagnostics of the collected
+        draws (the RCCL all-gather when N > 1). Returns this rank's figures;
+        main() aggregates."""
+        gm = self.gm
+        dt = np.float32 if cfg["dtype"] == "f32" else np.float64
+        C, D = cfg["chains"], cfg["dim"]
+        x0 = gm.init_with_seed(C, D, 42, np.float64, row0=offset).astype(dt)
+        if cfg["kind"] == "nuts":
+            mean, cov = dense_gauss_32()
+            s = gm.NUTS(gm.DenseGaussian(mean, cov), x0, cfg["target_accept"], dtype=dt,
+                        max_depth=cfg["max_depth"], chain_offset=offset).set_seed(42)
+        elif cfg["kind"] == "hmc":
+            s = gm.HMC(gm.RosenbrockND(), x0, cfg["eps"], cfg["L"], dtype=dt, chain_offset=offset).set_seed(42)
+        else:
+            s = gm.MetropolisHastings(gm.IsotropicGaussian(1.0), gm.IsotropicGaussian(cfg["proposal_std"]),
+                                      x0, dtype=dt, chain_offset=offset).seed(42)
+        try:
+            s.reserve(cfg["n_collect"])
+            lf0 = int(s.leapfrog_counts().sum())
+            self.sync()
+            self.cp.barrier()
+            t0 = time.perf_counter()
+            ds = s.run_positions(cfg["n_collect"], cfg["n_discard"])
+            self.sync()
+            t_run = time.perf_counter() - t0
+            kernel_ms, launches = s.last_run_stats()
+            leapfrogs = int(s.leapfrog_counts().sum()) - lf0
+            accept = float(s.accept_counts().mean())
+            self.cp.barrier()
+            t0 = time.perf_counter()
+            rhat, ess = self.diagnostics(ds, comm)
+            t_diag = time.perf_counter() - t0
+        finally:
+            s.close()
+        return {"run_s": t_run, "kernel_ms": kernel_ms, "launches": launches, "leapfrogs": leapfrogs,
+                "accepts_per_chain": accept, "diag_s": t_diag, "rhat": rhat, "ess": ess}
 
     def sampler(self, x0, offset):
         a = self.a
@@ -185,13 +260,13 @@ class GpuBench:
             s.close()
         return t_sample, t_diag, rhat, ess
 
-    def north_star_check(self, chains=16384):
+    def north_star_check(self, chains=16384, offset=0):
         """BASELINE.json north_star's target shape: >= 10^4 chains of 64-D
         Rosenbrock HMC on one GPU (device time of one launch)."""
         a, gm = self.a, self.gm
         D, L, n = a.dim, a.leapfrog, 100
-        s = gm.HMC(gm.RosenbrockND(), gm.init_with_seed(chains, D, 43, np.float64).astype(self.dtype),
-                   a.eps, L, dtype=self.dtype).set_seed(43)
+        s = gm.HMC(gm.RosenbrockND(), gm.init_with_seed(chains, D, 43, np.float64, row0=offset).astype(self.dtype),
+                   a.eps, L, dtype=self.dtype, chain_offset=offset).set_seed(43)
         try:
             s.reserve(n)
             s.run_positions(0, 20)
@@ -356,6 +431,65 @@ def rhat_block(rhat):
             "max_abs_dev_from_1": fin(np.max(np.abs(stan - 1.0)))}
 
 
+def config_summary(name, cfg, figs, world, rhat, ess):
+    """Aggregate one config leg over the ranks (max time, summed work) with
+    its own roofline: the FP64/FP32 vector peak for NUTS / HMC (F_alg of
+    SURVEY 8(d)), the HBM-equivalent bytes for MH (its unit there)."""
+    t = max(f["run_s"] for f in figs)
+    kms = max(f["kernel_ms"] for f in figs)
+    D = cfg["dim"]
+    chains = cfg["chains"] * world
+    s_bytes = 4 if cfg["dtype"] == "f32" else 8
+    total = cfg["n_collect"] + cfg["n_discard"] - (1 if cfg["kind"] == "nuts" else 0)
+    out = {"workload": None, "chains_total": chains, "chains_per_gpu": cfg["chains"], "dim": D,
+           "dtype": cfg["dtype"], "n_discard": cfg["n_discard"], "n_collect": cfg["n_collect"],
+           "transitions": total, "wall_s": t, "kernel_ms": kms,
+           "launches": max(f["launches"] for f in figs), "diag_s": max(f["diag_s"] for f in figs),
+           "accepts_per_chain": float(np.mean([f["accepts_per_chain"] for f in figs]))}
+    if cfg["kind"] == "nuts":
+        lf = sum(f["leapfrogs"] for f in figs)
+        fa = 2 * D * D + 8 * D
+        tf = fa * (lf / world) / (kms * 1e-3) / 1e12
+        out.update(workload=f"NUTS DenseGaussian dim={D} f64, {chains} chains, target_accept "
+                            f"{cfg['target_accept']}, max_depth {cfg['max_depth']}, run({cfg['n_collect']}, "
+                            f"{cfg['n_discard']})",
+                   metric="leapfrog steps/s", value=lf / t, value_kernel=lf / world / (kms * 1e-3) * world,
+                   leapfrogs=lf, mean_tree_leapfrogs=lf / (chains * total),
+                   roofline={"bound": "valu_f64", "kernel": "nuts_kernel", "achieved": tf,
+                             "peak": VALU_F64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / VALU_F64_PEAK_TFLOPS,
+                             "flops_per_leapfrog": fa,
+                             "note": "F = 2D^2 + 8D per leapfrog (SURVEY 8(d)) x leapfrogs counted on the "
+                                     "device / the run's HIP-event kernel time (per GPU)"})
+    elif cfg["kind"] == "hmc":
+        work = chains * cfg["L"] * total
+        fa = f_alg_rosenbrock(D)
+        tf = fa * (work / world) / (kms * 1e-3) / 1e12
+        out.update(workload=f"HMC RosenbrockND dim={D} {cfg['dtype']}, {chains} chains, eps {cfg['eps']}, "
+                            f"L {cfg['L']}, run({cfg['n_collect']}, {cfg['n_discard']})",
+                   metric="chain-leapfrog steps/s", value=work / t, value_kernel=work / (kms * 1e-3),
+                   roofline={"bound": "valu", "kernel": "hmc_kernel", "achieved": tf, "peak": VALU_F32_PEAK_TFLOPS,
+                             "unit": "TFLOP/s", "frac": tf / VALU_F32_PEAK_TFLOPS, "flops_per_chain_leapfrog": fa})
+    else:
+        work = chains * total
+        b = (2 * D + 2) * s_bytes
+        gbs = b * (work / world) / (kms * 1e-3) / 1e9
+        out.update(workload=f"MH IsotropicGaussian(1) dim={D} f64, proposal sd {cfg['proposal_std']:.5f}, "
+                            f"{chains} chains, run({cfg['n_collect']}, {cfg['n_discard']})",
+                   metric="chain-steps/s", value=work / t, value_kernel=work / (kms * 1e-3),
+                   roofline={"bound": "valu", "kernel": "mh_kernel",
+                             "hbm_equivalent": {"achieved_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
+                                                "frac": gbs / HBM_PEAK_GBS, "bytes_per_chain_step": b},
+                             "note": "per coordinate-step one f64 Philox/Box-Muller normal and one IEEE "
+                                     "divide: VALU-bound; the HBM-equivalent is SURVEY 8(d)'s (2D+2)s bytes "
+                                     "per chain-step over the kernel time (per GPU)"})
+    out["ess_mean"] = fin(np.mean(ess))
+    out["ess_min"] = fin(np.min(ess))
+    out["ess_per_sec"] = fin(np.mean(ess) / t)
+    out["ess_min_per_sec"] = fin(np.min(ess) / t)
+    out["rhat"] = rhat_block(rhat)
+    return out
+
+
 def main(argv=None, backend=None):
     a = parse(argv)
     from general_mcmc_amd.distributed import ControlPlane, shard
@@ -379,17 +513,23 @@ def main(argv=None, backend=None):
     # the sample buffer is resident before the clock starts, like the state;
     # the W warm-up transitions collect into it (untimed)
     sampler.reserve(max(a.steps, a.warmup))
-    # device warm-up (untimed): two launches of the timed shape on a scratch
-    # sampler with its own chains and buffers, then the W warm-up transitions
-    # of the measured sampler right before the timed call. Without the scratch
-    # launches the first timed call of a process is ~10 us slower end to end
-    # than the ones after it, and with them placed after the W transitions it
-    # still is (tools/probe_bench_first.py, profiles/r02/first_call/). The
-    # measured chains are exactly W transitions from the start.
+    # device warm-up (untimed): launches of the timed shape on a scratch
+    # sampler with its own chains and buffers for --device-warmup-ms (at
+    # least two), then the W warm-up transitions of the measured sampler right
+    # before the timed call. The GPU clock ramps to its peak only after ~10-30
+    # ms of load: after 0.2 ms of warm-up launches the timed 20-transition
+    # launch takes 103 us (2.26 GHz), after 30-100 ms 89.5 us
+    # (tools/probe_warmup.py, profiles/r03/warmup_probe.json); without the
+    # scratch launches the first call of a process is slower still
+    # (profiles/r02/first_call/). The measured chains are exactly W
+    # transitions from the start.
     scratch = be.sampler(x0, offset)
     scratch.reserve(a.steps)
-    for _ in range(2):
+    t_warm_end = time.perf_counter() + a.device_warmup_ms * 1e-3
+    n_scratch = 0
+    while n_scratch < 2 or time.perf_counter() < t_warm_end:
         scratch.run_positions(a.steps, 0)
+        n_scratch += 1
     if a.warmup > 0:
         sampler.run_positions(a.warmup, 0)
     barrier_sync()
@@ -430,6 +570,14 @@ def main(argv=None, backend=None):
                       "ess_min_per_sec_sampling": fin(np.min(es) / ts),
                       "ess_per_sec_end_to_end": fin(np.mean(es) / (ts + tdg)),
                       "rhat": rhat_block(rh)}
+    # the other BASELINE configs (every rank, its share; diagnostics over all)
+    configs = {}
+    for name in [c for c in a.configs.split(",") if c]:
+        cfg = CONFIG_LEGS[name]
+        off, _ = shard(cfg["chains"] * world, world, rank)
+        figs = be.config_leg(name, cfg, off, comm)
+        rh, es = figs.pop("rhat"), figs.pop("ess")
+        configs[name] = config_summary(name, cfg, cp.gather(figs), world, rh, es)
     comm_info = comm.info() if comm is not None else None
 
     # rank-0-only measurements; the other ranks wait at the closing barrier
@@ -438,7 +586,7 @@ def main(argv=None, backend=None):
         extra["copy_ceiling_gbs"] = be.copy_ceiling()
         extra["per_leapfrog_hbm"] = be.per_leapfrog_hbm()
         extra["host_output"] = be.host_output(sampler)
-        extra["north_star_check"] = be.north_star_check() if a.north_star else None
+        extra["north_star_check"] = be.north_star_check(offset=offset) if a.north_star else None
         extra["cpu_baseline"] = be.cpu_baseline(x0, lanes, elems) if a.cpu_seconds > 0 else None
     cp.barrier()
 
@@ -470,8 +618,9 @@ def main(argv=None, backend=None):
                        "layout": f"{lanes}x{elems}", "parallelism": f"chains sharded x{world}"},
             "timing": {"wall_ms": t_max * 1e3, "kernel_ms": kmax, "launches": launches,
                        "host_overhead_ms": t_max * 1e3 - kmax, "per_rank": ranks,
-                       "device_warmup": "two untimed launches of the timed shape on a scratch sampler (own chains "
-                                        "and buffers), then the W warm-up transitions of the measured sampler",
+                       "device_warmup": f"{n_scratch} untimed launches of the timed shape on a scratch sampler (own "
+                                        f"chains and buffers) for {a.device_warmup_ms:g} ms (GPU clock ramp), then "
+                                        "the W warm-up transitions of the measured sampler",
                        "note": "wall = barrier-bracketed timed region (max over ranks); kernel = HIP events "
                                "around the run's launches on the sampler's stream; host_overhead = wall - kernel"},
             "ess_per_sec": legs.get("cfg2_schedule", {}).get("ess_per_sec_sampling"),
@@ -502,6 +651,7 @@ def main(argv=None, backend=None):
                          "copy_ceiling_gbs": extra.get("copy_ceiling_gbs"),
                          "per_leapfrog_hbm": extra.get("per_leapfrog_hbm")},
             "cpu_baseline": extra.get("cpu_baseline"),
+            "configs": configs,
             "rccl": comm_info,
             "north_star_check": extra.get("north_star_check"),
             "host_output": extra.get("host_output"),

@@ -67,6 +67,7 @@ SIGNATURES = {
     "gm_device_synchronize": (_ip, []),
     "gm_gauss_from_cov": (_ip, [_i64, _vp, _vp, _vp]),
     "gm_init_positions": (_ip, [_u64, _i64, _i64, _ip, _vp]),
+    "gm_init_positions_rows": (_ip, [_u64, _i64, _i64, _i64, _ip, _vp]),
     "gm_target_logp_grad": (_ip, [C.POINTER(gm_target), _ip, _i64, _vp, _vp, _vp]),
     "gm_custom_target_check": (_ip, [C.c_char_p, _ip, _i64, _i32]),
     "gm_hmc_create": (_ip, [C.POINTER(gm_target), _ip, _i64, _i64, _vp, _dbl, _i64, _i64, C.POINTER(_vp)]),
@@ -92,6 +93,8 @@ SIGNATURES = {
     "gm_sampler_set_layout": (_ip, [_vp, _i32, _i32]),
     "gm_sampler_last_run_stats": (_ip, [_vp, C.POINTER(_dbl), C.POINTER(_i64)]),
     "gm_sampler_set_steps_per_launch": (_ip, [_vp, _i64]),
+    "gm_sampler_set_async": (_ip, [_vp, _i32]),
+    "gm_sampler_synchronize": (_ip, [_vp]),
     "gm_sampler_reserve": (_ip, [_vp, _i64]),
     "gm_state_size": (_ip, [_vp, C.POINTER(_u64)]),
     "gm_state_save": (_ip, [_vp, _vp, _u64]),

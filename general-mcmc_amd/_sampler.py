@@ -45,6 +45,7 @@ class DeviceSamples:
 
     def split_rhat_ess(self):
         self._check_live()
+        self.owner.synchronize()  # an asynchronous run may still be writing them
         return split_rhat_mean_ess_device(self.ptr, self.dtype, self.n_chains, self.n_collect,
                                           self.dim, (self.dim, self.n_chains * self.dim, 1))
 
@@ -201,6 +202,16 @@ class Sampler:
         self._gen += 1
         _lib.check(self._lib.gm_sampler_reserve(self._h, n_collect))
         return self
+
+    def set_async(self, on: bool = True):
+        """HMC / MH: run_positions and step return once the kernels are
+        enqueued; call synchronize() (or gm_device_synchronize) before using
+        the samples elsewhere (gm_sampler_set_async)."""
+        _lib.check(self._lib.gm_sampler_set_async(self._h, 1 if on else 0))
+        return self
+
+    def synchronize(self):
+        _lib.check(self._lib.gm_sampler_synchronize(self._h))
 
     def set_steps_per_launch(self, n: int):
         _lib.check(self._lib.gm_sampler_set_steps_per_launch(self._h, n))

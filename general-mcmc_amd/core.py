@@ -14,10 +14,12 @@ import numpy as np
 from . import _lib
 
 
-def init_with_seed(n: int, d: int, seed: int, dtype=np.float64) -> np.ndarray:
+def init_with_seed(n: int, d: int, seed: int, dtype=np.float64, row0: int = 0) -> np.ndarray:
+    """Rows [row0, row0 + n) of the seeded start (row0 > 0: a shard of a
+    larger global start, identical to slicing it)."""
     out = np.empty((n, d), dtype=dtype)
     lib = _lib.load()
-    _lib.check(lib.gm_init_positions(seed, n, d, _lib.dtype_code(dtype), _lib.ptr(out)))
+    _lib.check(lib.gm_init_positions_rows(seed, row0, n, d, _lib.dtype_code(dtype), _lib.ptr(out)))
     return out
 
 

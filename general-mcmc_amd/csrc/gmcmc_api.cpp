@@ -156,6 +156,8 @@ struct gm_sampler {
   double last_ms = 0;
   long long last_launches = 0;
   bool last_ms_pending = false;  // HMC/MH: last_ms is read from evs[0..1] on request
+  bool async_runs = false;       // HMC/MH runs return after enqueueing (gm_sampler_set_async)
+  bool may_async = false;        // set by the entry points that honour async_runs
   long long total_steps = 0;  // transitions since creation
   long long last_rows = 0;    // sample rows produced by the last run
   NutsState nuts;
@@ -383,16 +385,35 @@ int gm_gauss_from_cov(int64_t dim, const double* cov, double* prec, double* nc) 
   return GM_OK;
 }
 
-int gm_init_positions(uint64_t seed, int64_t n, int64_t dim, gm_dtype dtype, void* out) {
-  GM_REQ(n >= 0 && dim >= 0 && (out || n * dim == 0), "bad arguments");
+int gm_init_positions_rows(uint64_t seed, int64_t row0, int64_t n, int64_t dim, gm_dtype dtype, void* out) {
+  GM_REQ(n >= 0 && dim >= 0 && row0 >= 0 && (out || n * dim == 0), "bad arguments");
+  GM_REQ(row0 + n <= 0x100000000LL, "row ids must fit in 32 bits");
   GM_REQ(dtype == GM_F32 || dtype == GM_F64, "bad dtype");
-  for (int64_t i = 0; i < n; ++i)
-    for (int64_t d = 0; d < dim; ++d) {
-      const double z = normal<double>(seed, (uint32_t)i, 0, TAG_INIT, (uint32_t)d);
-      if (dtype == GM_F32) ((float*)out)[i * dim + d] = (float)z;
-      else ((double*)out)[i * dim + d] = z;
-    }
+  // rows are independent (keyed by their global id): large requests are
+  // split over host threads (a 131,072 x 256 start is 33.5M draws)
+  auto rows = [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i)
+      for (int64_t d = 0; d < dim; ++d) {
+        const double z = normal<double>(seed, (uint32_t)(row0 + i), 0, TAG_INIT, (uint32_t)d);
+        if (dtype == GM_F32) ((float*)out)[i * dim + d] = (float)z;
+        else ((double*)out)[i * dim + d] = z;
+      }
+  };
+  const int64_t work = n * dim;
+  int nt = work >= (1 << 20) ? (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency())) : 1;
+  if (nt > n) nt = (int)std::max<int64_t>(1, n);
+  if (nt <= 1) {
+    rows(0, n);
+    return GM_OK;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) th.emplace_back(rows, n * t / nt, n * (t + 1) / nt);
+  for (auto& x : th) x.join();
   return GM_OK;
+}
+
+int gm_init_positions(uint64_t seed, int64_t n, int64_t dim, gm_dtype dtype, void* out) {
+  return gm_init_positions_rows(seed, 0, n, dim, dtype, out);
 }
 
 int gm_target_logp_grad(const gm_target* target, gm_dtype dtype, int64_t n, const void* x,
@@ -566,6 +587,19 @@ int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems) {
   return GM_OK;
 }
 
+int gm_sampler_set_async(gm_sampler* s, int32_t on) {
+  GM_REQ(s, "sampler is NULL");
+  s->async_runs = on != 0;
+  return GM_OK;
+}
+
+int gm_sampler_synchronize(gm_sampler* s) {
+  GM_REQ(s, "sampler is NULL");
+  GM_HIP(hipSetDevice(s->device));
+  GM_HIP(hipStreamSynchronize(s->stream));
+  return GM_OK;
+}
+
 int gm_sampler_set_steps_per_launch(gm_sampler* s, int64_t steps) {
   GM_REQ(s, "sampler is NULL");
   // the kernels take a launch's transition count as an int
@@ -585,6 +619,7 @@ int gm_sampler_last_run_stats(gm_sampler* s, double* kernel_ms, int64_t* launche
   GM_REQ(s, "sampler is NULL");
   if (s->last_ms_pending) {  // the run's event pair, read only when asked for (off the run's path)
     float t = 0;
+    GM_HIP(hipEventSynchronize(s->evs[1]));  // an asynchronous run may still be in flight
     GM_HIP(hipEventElapsedTime(&t, s->evs[0], s->evs[1]));
     s->last_ms = t;
     s->last_ms_pending = false;
@@ -722,7 +757,7 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
   }
   s->step += total;
   s->total_steps += total;
-  GM_HIP(hipStreamSynchronize(s->stream));
+  if (!(s->async_runs && s->may_async)) GM_HIP(hipStreamSynchronize(s->stream));
   s->last_ms_pending = true;
   s->last_launches = n_launch;
   return GM_OK;
@@ -747,7 +782,10 @@ static int run_impl(gm_sampler* s, int64_t n_collect, int64_t n_discard, int pro
 }
 
 int gm_run_device(gm_sampler* s, int64_t n_collect, int64_t n_discard, const void** dev_samples) {
+  GM_REQ(s, "sampler is NULL");
+  s->may_async = true;  // the samples stay on the device: the caller may wait later
   int rc = run_impl(s, n_collect, n_discard, 0);
+  s->may_async = false;
   if (rc) return rc;
   if (dev_samples) *dev_samples = s->d_samples;
   return GM_OK;
@@ -1016,7 +1054,10 @@ int gm_sampler_chain_stats(gm_sampler* s, uint64_t* n, float* p_accept, float* m
 // init_chain_state, exactly as the reference's step() does.
 int gm_step(gm_sampler* s) {
   GM_REQ(s, "sampler is NULL");
-  return run_steps(s, 1, 1, s->kind == K_NUTS ? 2 : 0);
+  s->may_async = true;
+  const int rc = run_steps(s, 1, 1, s->kind == K_NUTS ? 2 : 0);
+  s->may_async = false;
+  return rc;
 }
 
 int gm_get_positions(gm_sampler* s, void* out) {

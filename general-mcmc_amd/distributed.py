@@ -104,6 +104,7 @@ class Comm:
         """Diagnostics of the union of all ranks' chains from each rank's
         DeviceSamples ([n_collect][C_local][dim] on its GPU)."""
         ds._check_live()
+        ds.owner.synchronize()  # an asynchronous run may still be writing them
         rhat = np.empty(ds.dim, dtype=np.float32)
         ess = np.empty(ds.dim, dtype=np.float32)
         _lib.check(self.lib.gm_split_rhat_ess_dist(
@@ -126,6 +127,7 @@ def split_rhat_ess_shards(shards) -> tuple[np.ndarray, np.ndarray]:
     d0 = shards[0]
     for d in shards:
         d._check_live()
+        d.owner.synchronize()
         if (d.n_chains, d.n_collect, d.dim, np.dtype(d.dtype)) != (d0.n_chains, d0.n_collect, d0.dim,
                                                                    np.dtype(d0.dtype)):
             raise ValueError("shards must have equal chain counts, draws, dims and dtypes")

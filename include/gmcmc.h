@@ -106,6 +106,9 @@ int gm_target_logp_grad(const gm_target* target, gm_dtype dtype, int64_t n, cons
  * analogue: same distribution and row-by-row meaning, not the same numbers,
  * see gm_rng.h). Host-side; out is [n][dim] of dtype. */
 int gm_init_positions(uint64_t seed, int64_t n, int64_t dim, gm_dtype dtype, void* out);
+/* Rows [row0, row0 + n) of the same stream (a shard's block of a global
+ * start: rank r of a sharded run takes rows [offset_r, offset_r + n_r)). */
+int gm_init_positions_rows(uint64_t seed, int64_t row0, int64_t n, int64_t dim, gm_dtype dtype, void* out);
 
 /* ---- device / errors ------------------------------------------------ */
 const char* gm_last_error(void);
@@ -241,6 +244,17 @@ int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems);
 /* Device time (ms) of the sampling kernels launched by the last run, and the
  * number of launches (HIP events on the sampler's stream). */
 int gm_sampler_last_run_stats(gm_sampler* s, double* kernel_ms, int64_t* launches);
+
+/* Asynchronous runs (HMC and MH samplers; NUTS runs stay synchronous):
+ * with on != 0, gm_run_device / gm_step return once the sampler's kernels
+ * are enqueued on its stream instead of waiting for them. The caller then
+ * waits with gm_sampler_synchronize or gm_device_synchronize before reading
+ * the samples from another stream (the diagnostics, gm_memcpy_*); the
+ * sampler's own calls (copies, positions, state) are ordered after the run
+ * on its stream. A benchmark that brackets a run with device synchronizes
+ * uses it to wait once instead of twice. */
+int gm_sampler_set_async(gm_sampler* s, int32_t on);
+int gm_sampler_synchronize(gm_sampler* s);
 
 /* Transitions per kernel launch (state stays in registers inside a launch). */
 int gm_sampler_set_steps_per_launch(gm_sampler* s, int64_t steps);

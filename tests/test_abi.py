@@ -67,6 +67,15 @@ def test_init_positions_match_oracle_stream(oracle):
     assert g.init_det(3, 4, np.float32).dtype == np.float32
 
 
+def test_init_positions_rows_are_a_slice_of_the_global_start():
+    """A shard's rows (gm_init_positions_rows) equal the same rows of the
+    whole start, including the multi-threaded path (>= 2^20 draws)."""
+    import general_mcmc_amd as g
+    full = g.init_with_seed(4200, 256, 42)
+    np.testing.assert_array_equal(g.init_with_seed(1000, 256, 42, row0=3000)[:1000], full[3000:4000])
+    np.testing.assert_array_equal(g.init_with_seed(7, 256, 42, row0=13), full[13:20])
+
+
 def test_no_silent_cpu_fallback_without_gpu():
     """Without a visible GPU the samplers must raise, never compute elsewhere."""
     import general_mcmc_amd as g

@@ -94,8 +94,14 @@ def stub_backend():
         def host_output(self, sampler):
             return {"chain_leapfrogs_per_s": 1.0}
 
-        def north_star_check(self):
+        def north_star_check(self, offset=0):
             return None
+
+        def config_leg(self, name, cfg, offset, comm):
+            r, e = self.diagnostics(_Samples(cfg["n_collect"], cfg["chains"], cfg["dim"]), comm)
+            k = 1 + self.cp.rank  # rank 1 is the slower one
+            return {"run_s": 0.1 * k, "kernel_ms": 50.0 * k, "launches": 1, "leapfrogs": 1000 * cfg["chains"],
+                    "accepts_per_chain": 10.0, "diag_s": 0.01, "rhat": r, "ess": e}
 
         def cpu_baseline(self, x0, lanes, elems):
             return bench.cpu_baseline(self.a, np.float32, x0, lanes, elems)
@@ -149,3 +155,14 @@ def test_bench_line_world1_and_world2(tmp_path):
         assert line["ess"]["cfg2_schedule"]["rhat"]["stan_sqrt_V_over_W"]["max"] > 1.0
     # the ESS legs time the slowest rank
     assert l2["ess"]["cfg2_schedule"]["sampling_s"] == 0.02
+    # the config legs: every rank's share, the slowest rank's time, work summed
+    for line, world in ((l1, 1), (l2, 2)):
+        assert set(line["configs"]) == {"cfg3", "cfg4", "cfg5"}
+        c3 = line["configs"]["cfg3"]
+        assert c3["chains_total"] == 8192 * world and c3["leapfrogs"] == 1000 * 8192 * world
+        assert c3["wall_s"] == 0.1 * world and c3["value"] == c3["leapfrogs"] / c3["wall_s"]
+        assert c3["roofline"]["bound"] == "valu_f64" and c3["roofline"]["frac"] > 0
+        c5 = line["configs"]["cfg5"]
+        assert c5["value"] == 16384 * world * 1100 / (0.1 * world)
+        assert c5["roofline"]["hbm_equivalent"]["frac"] > 0
+        assert line["configs"]["cfg4"]["transitions"] == 200

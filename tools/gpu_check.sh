@@ -27,6 +27,10 @@ for step in "$@"; do
     diagtest) run diag_tests 600 python -u -m pytest tests/test_gpu_diag_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
     abmh) AB_ROUNDS=${AB_ROUNDS:-3} run ab_mh 600 python tools/ab_mh.py ${AB_LIBS} ;;
     abnuts) AB_ROUNDS=${AB_ROUNDS:-3} run ab_nuts 900 python tools/ab_nuts.py ${AB_LIBS} ;;
+    warmup) run warmup_probe 300 python tools/probe_warmup.py ;;
+    hostpath) run host_path 120 python tools/probe_host_path.py ;;
+    steptests) run step_tests 300 python -u -m pytest tests/test_gpu_step.py -x -v --timeout 120 --timeout-method thread ;;
+    benchn) run bench_new 600 python bench.py --steps 20 --warmup 5 ;;
     smoke) run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench20) run bench20 300 python bench.py --steps 20 --warmup 5 ;;
     bench) run bench 300 python bench.py ;;
