@@ -36,7 +36,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 VALU_F32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md, spec)
 VALU_F64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (MI355X_MICROARCH.md, spec)
 METRIC = "leapfrog steps/sec (whole node) + ESS/sec, 64-dim Rosenbrock HMC at 1/2/4/8 GPUs"
-PMC_FILE = os.path.join(ROOT, "profiles", "r02", "pmc_hmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_hmc.json")
 
 
 def parse(argv=None):
@@ -152,7 +152,26 @@ class GpuBench:
             self.sync()
             self.cp.barrier()
             t0 = time.perf_counter()
-            ds = s.run_positions(cfg["n_collect"], cfg["n_discard"])
+            warm = None
+            if cfg["kind"] == "nuts":
+                # NUTS::run(n_collect, n_discard) as its two phases: run(1,
+                # n_discard) adapts the step size over the n_discard warm-up
+                # transitions, then run(n_collect, 0) takes the n_collect - 1
+                # sampling transitions at eps_bar (row 0 = the warm-up's end
+                # state): the same 999 transitions and rows as the single
+                # call (nuts.rs:232-257; generic_nuts.rs:882-924), with the
+                # sampling phase timed on its own
+                s.run_positions(1, cfg["n_discard"])
+                self.sync()
+                t_w = time.perf_counter() - t0
+                kms_w, _ = s.last_run_stats()
+                lf_w = int(s.leapfrog_counts().sum()) - lf0
+                warm = {"warmup_s": t_w, "warmup_kernel_ms": kms_w, "warmup_leapfrogs": lf_w}
+                lf0 += lf_w
+                t0 = time.perf_counter()
+                ds = s.run_positions(cfg["n_collect"], 0)
+            else:
+                ds = s.run_positions(cfg["n_collect"], cfg["n_discard"])
             self.sync()
             t_run = time.perf_counter() - t0
             kernel_ms, launches = s.last_run_stats()
@@ -164,8 +183,11 @@ class GpuBench:
             t_diag = time.perf_counter() - t0
         finally:
             s.close()
-        return {"run_s": t_run, "kernel_ms": kernel_ms, "launches": launches, "leapfrogs": leapfrogs,
-                "accepts_per_chain": accept, "diag_s": t_diag, "rhat": rhat, "ess": ess}
+        out = {"run_s": t_run, "kernel_ms": kernel_ms, "launches": launches, "leapfrogs": leapfrogs,
+               "accepts_per_chain": accept, "diag_s": t_diag, "rhat": rhat, "ess": ess}
+        if warm:
+            out.update(warm)
+        return out
 
     def sampler(self, x0, offset):
         a = self.a
@@ -448,13 +470,21 @@ def config_summary(name, cfg, figs, world, rhat, ess):
            "accepts_per_chain": float(np.mean([f["accepts_per_chain"] for f in figs]))}
     if cfg["kind"] == "nuts":
         lf = sum(f["leapfrogs"] for f in figs)
+        lf_w = sum(f.get("warmup_leapfrogs", 0) for f in figs)
+        t_w = max(f.get("warmup_s", 0.0) for f in figs)
+        n_samp = cfg["n_collect"] - 1
         fa = 2 * D * D + 8 * D
         tf = fa * (lf / world) / (kms * 1e-3) / 1e12
         out.update(workload=f"NUTS DenseGaussian dim={D} f64, {chains} chains, target_accept "
                             f"{cfg['target_accept']}, max_depth {cfg['max_depth']}, run({cfg['n_collect']}, "
-                            f"{cfg['n_discard']})",
-                   metric="leapfrog steps/s", value=lf / t, value_kernel=lf / world / (kms * 1e-3) * world,
-                   leapfrogs=lf, mean_tree_leapfrogs=lf / (chains * total),
+                            f"{cfg['n_discard']}) as run(1, {cfg['n_discard']}) + run({cfg['n_collect']}, 0)",
+                   metric="leapfrog steps/s (sampling phase)", value=lf / t, value_kernel=lf / (kms * 1e-3),
+                   leapfrogs=lf, mean_tree_leapfrogs=lf / (chains * n_samp),
+                   sampling_transitions=n_samp, sampling_s=t,
+                   warmup={"transitions": cfg["n_discard"], "wall_s": t_w, "leapfrogs": lf_w,
+                           "kernel_ms": max(f.get("warmup_kernel_ms", 0.0) for f in figs),
+                           "leapfrogs_per_s": lf_w / t_w if t_w > 0 else None},
+                   whole_run={"wall_s": t + t_w, "leapfrogs_per_s": (lf + lf_w) / (t + t_w)},
                    roofline={"bound": "valu_f64", "kernel": "nuts_kernel", "achieved": tf,
                              "peak": VALU_F64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / VALU_F64_PEAK_TFLOPS,
                              "flops_per_leapfrog": fa,

@@ -100,8 +100,11 @@ def stub_backend():
         def config_leg(self, name, cfg, offset, comm):
             r, e = self.diagnostics(_Samples(cfg["n_collect"], cfg["chains"], cfg["dim"]), comm)
             k = 1 + self.cp.rank  # rank 1 is the slower one
-            return {"run_s": 0.1 * k, "kernel_ms": 50.0 * k, "launches": 1, "leapfrogs": 1000 * cfg["chains"],
-                    "accepts_per_chain": 10.0, "diag_s": 0.01, "rhat": r, "ess": e}
+            out = {"run_s": 0.1 * k, "kernel_ms": 50.0 * k, "launches": 1, "leapfrogs": 1000 * cfg["chains"],
+                   "accepts_per_chain": 10.0, "diag_s": 0.01, "rhat": r, "ess": e}
+            if cfg["kind"] == "nuts":
+                out.update(warmup_s=0.05 * k, warmup_kernel_ms=40.0 * k, warmup_leapfrogs=900 * cfg["chains"])
+            return out
 
         def cpu_baseline(self, x0, lanes, elems):
             return bench.cpu_baseline(self.a, np.float32, x0, lanes, elems)
@@ -162,6 +165,7 @@ def test_bench_line_world1_and_world2(tmp_path):
         assert c3["chains_total"] == 8192 * world and c3["leapfrogs"] == 1000 * 8192 * world
         assert c3["wall_s"] == 0.1 * world and c3["value"] == c3["leapfrogs"] / c3["wall_s"]
         assert c3["roofline"]["bound"] == "valu_f64" and c3["roofline"]["frac"] > 0
+        assert c3["warmup"]["leapfrogs"] == 900 * 8192 * world and c3["warmup"]["wall_s"] == 0.05 * world
         c5 = line["configs"]["cfg5"]
         assert c5["value"] == 16384 * world * 1100 / (0.1 * world)
         assert c5["roofline"]["hbm_equivalent"]["frac"] > 0

@@ -10,15 +10,19 @@ command, one run per pass, each pass in its own directory under PROF_DIR:
                 SQ_ACTIVE_INST_VALU SQ_WAIT_ANY
   grbm/   --pmc GRBM_GUI_ACTIVE       (GPU busy cycles, summed over 8 XCDs)
 
+  flops/  --pmc SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 (optional)
+
 The dispatch is selected by kernel name AND grid size (threads), then by its
-ordinal among the dispatches that match both (default: the bench's timed
-launch, the 4th dispatch of the bench's grid: two scratch warm-up launches
-and the W warm-up transitions precede it). Other kernels of the same name
-(the config legs, the north-star shape) have other grids, so they never
-shift the ordinal.
+ordinal among the dispatches that match both. The bench's timed launch is
+the 4th from the END of the bench's grid (tools/profile_r03.sh runs bench.py
+with --ess-long-discard 0 --no-north-star --cpu-seconds 0): the cfg2 ESS leg
+and the two host-output launches follow it, while the time-based scratch
+warm-up puts a varying number of launches before it. Other kernels of the
+same name (the cfg4 leg, the north-star shape) have other grids, so they
+never shift the ordinal.
 
     python tools/pmc_dispatch.py PROF_DIR --kernel hmc_kernel --grid 262144 \
-        --ordinal 3 --key C4096_D64_L50_f32 --steps 20 --out profiles/r03/pmc_hmc.json
+        --ordinal -4 --key C4096_D64_L50_f32 --steps 20 --out profiles/r03/pmc_hmc.json
 """
 import argparse
 import collections
@@ -74,6 +78,16 @@ def measure(prof_dir, kernel, grid, ordinal, simds=1024):
     grbm, _ = counters(os.path.join(prof_dir, "grbm"), kernel, grid, ordinal)
     cycles = grbm["GRBM_GUI_ACTIVE"] / 8.0
     waves = max(sq["SQ_WAVES"], 1)
+    flops = None
+    fdir = os.path.join(prof_dir, "flops")
+    if os.path.isdir(fdir):
+        fl, _ = counters(fdir, kernel, grid, ordinal)
+        # SQ_INSTS_VALU_FLOPS_* count per wave instruction (the lanes' flops
+        # / 64): x 64 gives lane flops, comparable with F_alg
+        flops = {"fp32_lane_flops": 64.0 * fl.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0),
+                 "fp64_lane_flops": 64.0 * fl.get("SQ_INSTS_VALU_FLOPS_FP64", 0.0),
+                 "note": "SQ_INSTS_VALU_FLOPS_FP32/FP64 x 64 (the counter's unit is per wave instruction, "
+                         "1/64 of the lanes' flops)"}
     return {
         "kernel": meta.get("kernel_name"), "grid_threads": grid, "ordinal": ordinal,
         "launch_us_traced": dur * 1e6,
@@ -90,6 +104,7 @@ def measure(prof_dir, kernel, grid, ordinal, simds=1024):
                     "GRBM_GUI_ACTIVE/8); per-wave counts are SQ_INSTS_* / SQ_WAVES",
         },
         "registers": meta,
+        "pmc_flops": flops,
         "correction": "HBM bytes = FETCH_SIZE x 2 (gfx950 half count) + WRITE_SIZE, KB = 1024 B",
         "source": f"{prof_dir}: trace, fetch, write, sq, grbm passes (rocprofv3, one run each); "
                   f"{kernel} dispatch #{ordinal} of grid {grid}",
@@ -101,7 +116,7 @@ def main():
     ap.add_argument("prof_dir")
     ap.add_argument("--kernel", default="hmc_kernel")
     ap.add_argument("--grid", type=int, required=True, help="Grid_Size in threads")
-    ap.add_argument("--ordinal", type=int, default=3)
+    ap.add_argument("--ordinal", type=int, default=-4)
     ap.add_argument("--key", required=True)
     ap.add_argument("--steps", type=int, default=0, help="transitions of the launch (HMC fit)")
     ap.add_argument("--out", required=True)
