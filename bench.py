@@ -383,6 +383,17 @@ def cpu_baseline(a, dtype, x0, lanes, elems):
         out["value"] = C * a.leapfrog * steps / dt
         out["sample"] = (f"{C} chains x {steps} transitions x {a.leapfrog} leapfrogs, oracle/cpu_hmc.c "
                          f"(-O3 -march=native, reference op structure), {threads} threads, {dt:.1f}s")
+        # the same restatement on one core (BASELINE.md section 3 asks for 1 thread and all cores)
+        t0 = time.perf_counter()
+        fast.run(q, a.eps, a.leapfrog, 1, 44, 1)
+        one1 = time.perf_counter() - t0
+        steps1 = max(1, int(0.5 * a.cpu_seconds / max(one1, 1e-6)))
+        t0 = time.perf_counter()
+        fast.run(q, a.eps, a.leapfrog, steps1, 45, 1)
+        dt1 = time.perf_counter() - t0
+        out["one_thread"] = {"value": C * a.leapfrog * steps1 / dt1, "cores": 1,
+                             "sample": f"{C} chains x {steps1} transitions x {a.leapfrog} leapfrogs, "
+                                       f"oracle/cpu_hmc.c, 1 thread, {dt1:.1f}s"}
     ora = _oracle.load()
     t = _oracle.Target(1, a.dim, a=1.0, b=100.0)
     q = np.array(x0, copy=True)

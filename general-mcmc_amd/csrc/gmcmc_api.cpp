@@ -22,6 +22,8 @@
 #include <thread>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "gm_jit.h"
 #include "gm_layouts.h"
 #include "gm_nuts.h"
@@ -119,6 +121,27 @@ using namespace gm;
   } while (0)
 
 enum SamplerKind { K_HMC = 1, K_MH = 2, K_NUTS = 3 };
+
+// roctx ranges around the sampler entry points (the
+// reference times its runs with dev_tools::Timer, here the ranges appear in
+// rocprofv3 --marker-trace timelines). Enabled by GMCMC_ROCTX=1 (read once),
+// so that the bench's timed call carries no annotation cost by default.
+static bool roctx_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("GMCMC_ROCTX");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+struct RoctxRange {
+  bool on;
+  explicit RoctxRange(const char* name) : on(roctx_on()) {
+    if (on) roctxRangePushA(name);
+  }
+  ~RoctxRange() {
+    if (on) roctxRangePop();
+  }
+};
 
 struct gm_sampler {
   int kind = 0;
@@ -782,6 +805,7 @@ static int run_impl(gm_sampler* s, int64_t n_collect, int64_t n_discard, int pro
 }
 
 int gm_run_device(gm_sampler* s, int64_t n_collect, int64_t n_discard, const void** dev_samples) {
+  RoctxRange rr("gm_run_device");
   GM_REQ(s, "sampler is NULL");
   s->may_async = true;  // the samples stay on the device: the caller may wait later
   int rc = run_impl(s, n_collect, n_discard, 0);
@@ -895,6 +919,7 @@ int gm_copy_sample_block(gm_sampler* s, int64_t row0, int64_t n_rows, int64_t ch
 }
 
 int gm_run(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out) {
+  RoctxRange rr("gm_run");
   int rc = run_impl(s, n_collect, n_discard, 0);
   if (rc) return rc;
   if (!out || n_collect == 0) return GM_OK;
@@ -915,6 +940,7 @@ static float max_skipnan(const float* v, long long n) {  // stats.rs:154-161
 int gm_run_progress_cb(gm_sampler* s, int64_t n_collect, int64_t n_discard, void* out,
                        float* rhat_out, float* ess_out, gm_progress_fn cb, void* user,
                        double interval_s) {
+  RoctxRange rr("gm_run_progress");
   GM_REQ(s, "sampler is NULL");
   GM_REQ(n_collect >= 0 && n_discard >= 0, "n_collect and n_discard must be >= 0");
   GM_HIP(hipSetDevice(s->device));
@@ -1053,6 +1079,7 @@ int gm_sampler_chain_stats(gm_sampler* s, uint64_t* n, float* p_accept, float* m
 // completed run never is; then eps = eps_bar) and does not re-run
 // init_chain_state, exactly as the reference's step() does.
 int gm_step(gm_sampler* s) {
+  RoctxRange rr("gm_step");
   GM_REQ(s, "sampler is NULL");
   s->may_async = true;
   const int rc = run_steps(s, 1, 1, s->kind == K_NUTS ? 2 : 0);

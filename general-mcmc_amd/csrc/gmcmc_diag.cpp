@@ -5,11 +5,14 @@
 #include <rccl/rccl.h>
 
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <set>
 #include <string>
 #include <vector>
+
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "gm_diag.h"
 
@@ -86,6 +89,17 @@ struct gm_comm {
 static int local_diag(const void* dev_sample, gm_dtype dtype, int64_t C, int64_t N, int64_t P,
                       int64_t sc, int64_t sd, int64_t sp, gm_comm* comm, float* rhat_out,
                       float* ess_out, hipStream_t st) {
+  static const bool rtx = [] {  // GMCMC_ROCTX=1: a roctx range per diagnostic call
+    const char* e = std::getenv("GMCMC_ROCTX");
+    return e && e[0] == '1';
+  }();
+  struct R {
+    bool on;
+    ~R() {
+      if (on) roctxRangePop();
+    }
+  } rr{rtx};
+  if (rtx) roctxRangePushA(comm ? "gm_split_rhat_ess_dist" : "gm_split_rhat_ess");
   GM_REQ(dtype == GM_F32 || dtype == GM_F64, "bad dtype");
   GM_REQ(C >= 1 && N >= 2 && P >= 1, "need n_chains >= 1, n_draws >= 2, n_params >= 1");
   GM_REQ(dev_sample && rhat_out && ess_out, "NULL argument");

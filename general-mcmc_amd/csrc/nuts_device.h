@@ -335,7 +335,8 @@ __device__ __attribute__((noinline)) T find_reasonable_epsilon(const TG& tg, con
 // wave's chains did in it (bit 0 a transition start, 1 a subtree merge,
 // 2 a doubling end, 3 a transition end) plus the evaluation's share;
 // read back by gm_nuts_prof_read (nuts_kernels.hip).
-constexpr int NPROF_SLOTS = 16 * 2 + 3;
+// slots 35..42: cycles of the iteration's segments (see GM_PSEG below)
+constexpr int NPROF_SLOTS = 16 * 2 + 3 + 8;
 constexpr int NPROF_WAVES = 8192;
 __device__ unsigned long long gm_nuts_prof_buf[NPROF_WAVES * NPROF_SLOTS];
 #endif
@@ -529,6 +530,18 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
   }
 
 #ifdef GM_NUTS_PROF
+  // segments: 0 top -> after momentum draw, 1 -> after kick/drift, 2 -> after
+  // the target's eval_part, 3 -> after the second kick and kinetic part,
+  // 4 -> after the reduction, 5 -> after the leaf rules (joint, exp),
+  // 6 -> after the merge climb, 7 -> end of iteration (doubling / transition end)
+  unsigned long long pseg[8] = {}, pst = 0;
+#define GM_PSEG(i)                                                        \
+  do {                                                                    \
+    __builtin_amdgcn_s_waitcnt(0);                                        \
+    const unsigned long long _n = __builtin_amdgcn_s_memtime();           \
+    pseg[i] += _n - pst;                                                  \
+    pst = _n;                                                             \
+  } while (0)
   unsigned long long pcnt[16] = {}, pcyc[16] = {}, peval = 0, piter = 0;
   unsigned long long ptop = __builtin_amdgcn_s_memtime();
   bool f_start = false, f_merge = false, f_dbl = false, f_trans = false;
@@ -558,6 +571,8 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       }
       ++piter;
       ptop = now;
+      if (piter > 1) pseg[7] += now - pst;
+      pst = now;
       f_start = f_merge = f_dbl = f_trans = false;
     }
 #endif
@@ -572,10 +587,18 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int i = lane * E + e;
+#ifdef GM_KO_MOM  // measurement build only: a cheap unit-variance draw instead of Box-Muller
+        const uint32_t hh = (cid * 0x9E3779B1u) ^ ((uint32_t)st * 0x85EBCA77u) ^ ((uint32_t)i * 0xC2B2AE3Du);
+        z[e] = (i < D) ? ((T)((hh ^ (hh >> 15)) & 0xffffu) * (T)(1.0 / 65536.0) - (T)0.5) * (T)3.4641016 : (T)0;
+#else
         z[e] = (i < D) ? ncache[e].get(a.seed, cid, st, TAG_NUTS_MOM, (uint32_t)i) : (T)0;
+#endif
       }
       momentum_from<LPC, E>(M, z, p0, lane);
     }
+#ifdef GM_NUTS_PROF
+    GM_PSEG(0);
+#endif
     if constexpr (MASS == 0) {  // leapfrog (:1396-1418), as selects: kick, drift
       const bool adv = live && !starting;
 #pragma unroll
@@ -596,7 +619,13 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
 #pragma unroll
     for (int e = 0; e < E; ++e) x[e] = starting ? q[e] : qe[e];
     T sums[2];
+#ifdef GM_NUTS_PROF
+    GM_PSEG(1);
+#endif
     sums[0] = tg.template eval_part<LPC, E>(x, gx, lane);
+#ifdef GM_NUTS_PROF
+    GM_PSEG(2);
+#endif
     {
       const bool adv = live && !starting;
 #pragma unroll
@@ -611,7 +640,13 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       for (int e = 0; e < E; ++e) pk[e] = starting ? p0[e] : pe[e];
       sums[1] = kin_part_m<LPC, E>(M, pk, lane);
     }
+#ifdef GM_NUTS_PROF
+    GM_PSEG(3);
+#endif
     group_sum_n<LPC>(sums);  // log-density and kinetic energy, reduced together
+#ifdef GM_NUTS_PROF
+    GM_PSEG(4);
+#endif
 #ifdef GM_NUTS_PROF
     peval += __builtin_amdgcn_s_memtime() - ptop;
 #endif
@@ -649,10 +684,17 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     const T joint = lp - kin;
     tn = (logu < joint) ? 1 : 0;
     ts = (logu - (T)1000) < joint;
+#ifdef GM_KO_EXP  // measurement build only: the exp skipped past warm-up (h_bar then differs)
+    ta = (a.m0 + s + 1 <= a.n_discard) ? rust_min1(gexp(joint - joint0, ek)) : (T)1;
+#else
     ta = rust_min1(gexp(joint - joint0, ek));
+#endif
     tna = 1;
 #pragma unroll
     for (int e = 0; e < E; ++e) { fq[e] = qe[e]; fp[e] = pe[e]; pr[e] = qe[e]; }
+#ifdef GM_NUTS_PROF
+    GM_PSEG(5);
+#endif
     // climb: merge with the stored left siblings this leaf completes
     bool done = false;
     int k = 0;
@@ -676,12 +718,19 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       int ln_, lna;
       T lal;
       stack_scalars(k, lal, ln_, lna);
+#ifdef GM_KO_MERGE  // measurement build only: no hash draw, no division
+      const double u = 0.5;
+      ++merge_ctr;
+      {
+        const bool keep_left = !(u * (double)(ln_ + tn) < (double)tn);
+#else
       const double u = nuts_u<double>(key, 64u + merge_ctr++);
       const int den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
       // (selects rather than branches from here on: the chains of a wave
       // take different sides, and a divergent branch costs both)
       {
         const bool keep_left = !(u < (double)tn / (double)den);
+#endif
         T lpr[E];
         stack_vec(k, 2, lpr);
 #pragma unroll
@@ -706,6 +755,9 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       for (int e = 0; e < E; ++e) { fq[e] = lq[e]; fp[e] = lpv[e]; }
       ++k;
     }
+#ifdef GM_NUTS_PROF
+    GM_PSEG(6);
+#endif
     if (!done) {
       ++l;
       continue;
@@ -819,6 +871,7 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
       unsigned long long pprod = 0;  // cycles inside the target's matrix-core product, if it has one
       if constexpr (requires { tg.prof_prod; }) pprod = tg.prof_prod;
       o[34] = pprod;
+      for (int b = 0; b < 8; ++b) o[35 + b] = pseg[b];
     }
   }
 #endif

@@ -154,6 +154,7 @@ def test_bench_line_world1_and_world2(tmp_path):
         assert line["roofline"]["bound"] == "valu" and 0 < line["roofline"]["frac"]
         cb = line["cpu_baseline"]
         assert cb["cores"] >= 1 and cb["value"] > 0 and "sched_getaffinity" in cb["host"]
+        assert cb["one_thread"]["cores"] == 1 and cb["one_thread"]["value"] > 0
         assert set(line["ess"]) == {"cfg2_schedule", "long"}
         assert line["ess"]["cfg2_schedule"]["rhat"]["stan_sqrt_V_over_W"]["max"] > 1.0
     # the ESS legs time the slowest rank

@@ -27,6 +27,7 @@ for step in "$@"; do
     diagtest) run diag_tests 600 python -u -m pytest tests/test_gpu_diag_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
     abmh) AB_ROUNDS=${AB_ROUNDS:-3} run ab_mh 600 python tools/ab_mh.py ${AB_LIBS} ;;
     abnuts) AB_ROUNDS=${AB_ROUNDS:-3} run ab_nuts 900 python tools/ab_nuts.py ${AB_LIBS} ;;
+    nlevels) run nuts_levels 300 python tools/probe_nuts_levels.py ;;
     warmup) run warmup_probe 300 python tools/probe_warmup.py ;;
     hostpath) run host_path 120 python tools/probe_host_path.py ;;
     steptests) run step_tests 300 python -u -m pytest tests/test_gpu_step.py -x -v --timeout 120 --timeout-method thread ;;

@@ -36,7 +36,7 @@ def main():
     lib = gm._lib.load()
     lanes, elems = s.layout()
     waves = chains * lanes // 64
-    buf = np.zeros((waves, 35), np.uint64)
+    buf = np.zeros((waves, 43), np.uint64)
     f = lib.gm_nuts_prof_read
     f.argtypes = [C.c_void_p, C.c_longlong]
     assert f(buf.ctypes.data, buf.size) == 0
@@ -60,6 +60,12 @@ def main():
     coef, *_ = np.linalg.lstsq(X[w] * np.sqrt(cnt[w])[:, None], (cyc[w] / np.maximum(cnt[w], 1)) * np.sqrt(cnt[w]),
                                rcond=None)
     out["fit_cycles"] = {"base": coef[0], **{NAMES[i]: coef[i + 1] for i in range(4)}}
+    seg_names = ["momentum_draw", "kick_drift", "target_eval_part", "kick_kinetic_part", "reduction",
+                 "leaf_rules", "merge_climb", "doubling_transition_end"]
+    seg = buf[:, 35:43].astype(np.float64).sum(0) / it
+    out["segments_cycles_per_iteration"] = {n: float(v) for n, v in zip(seg_names, seg)}
+    out["segments_note"] = ("measurement build: an s_waitcnt(0) + s_memtime at each boundary, so memory "
+                            "latency is charged to the segment that issued the access")
     print(json.dumps(out, indent=1))
 
 
