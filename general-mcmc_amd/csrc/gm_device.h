@@ -193,6 +193,27 @@ template <class T> __device__ __forceinline__ T keep(T v, typename MaskOf<T>::ty
 __device__ __forceinline__ float gfma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 __device__ __forceinline__ double gfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
+// a / b for a divisor b fixed over a kernel, with y = RN(1/b) precomputed:
+// the IEEE quotient RN(a/b) in one multiply and four fused multiply-adds
+// instead of the ~10-instruction division sequence. q0 = RN(a y) is within
+// 1.5 ulp of a/b; one Newton-Markstein correction q1 = RN(q0 + RN(a - b q0) y)
+// (the remainder exact by fma) is faithful; a second one, q2, is then the
+// correctly rounded quotient (Markstein's theorem: y within half an ulp of
+// 1/b and a faithful q). The theorem excludes under/overflow and non-finite
+// a: those inputs (|a/b| outside [2^-1000, 2^1000], a = 0, inf, NaN) take
+// the IEEE division itself, in a branch no wave of the samplers reaches in
+// practice; a = 0 keeps its sign through that branch too.
+template <class T> __device__ __forceinline__ T div_by_const(T a, T b, T y) {
+  const T q0 = a * y;
+  const T q1 = gfma(gfma(-b, q0, a), y, q0);
+  const T q2 = gfma(gfma(-b, q1, a), y, q1);
+  const T m = q2 < (T)0 ? -q2 : q2;
+  constexpr T lo = sizeof(T) == 8 ? (T)9.332636185032189e-302 : (T)1e-30f;  // 2^-1000 | 1e-30
+  constexpr T hi = sizeof(T) == 8 ? (T)1.0715086071862673e+301 : (T)1e30f;  // 2^1000  | 1e30
+  if (__builtin_expect(!(m >= lo && m <= hi), 0)) return a / b;
+  return q2;
+}
+
 template <class T, int E> struct RosenbrockLane;
 template <class T> struct RosenbrockT {
   T a, b, b2, b4;  // b2 = 2b, b4 = 4b (rounded once, host side)

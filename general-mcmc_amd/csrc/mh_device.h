@@ -24,6 +24,7 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   const T sd = (T)a.prop_std;
   const T var = sd * sd;
   const T two_var = (T)2 * var;
+  const T inv_two_var = (T)1 / two_var;  // div_by_const: the exact quotient by two_var
   const T pi = (T)3.14159265358979323846;
   const T qconst = (-(T)D * (T)0.5) * glog(((var * pi) * sd) * sd);
 
@@ -37,6 +38,8 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   long long acc = 0;
   NormalCache<T> ncache[E];
   UniformCache<T> ucache;
+  uint64_t lblk = ~0ull;  // LPC == 64: the draw block whose accept logs lnl holds (lane k: step k)
+  T lnl = (T)0;
   const bool track = a.trk.mean != nullptr;  // run_progress (core.rs:146-163)
   ChainTrack<LPC, E> tr;
   if (track) tr.load(a.trk, c, lane, D);
@@ -53,13 +56,33 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
         y[e] = (T)0;
       }
       const T d = y[e] - x[e];
-      const T ex = (i < D) ? (-(d * d)) / two_var : (T)0;
+      // -(d*d) / two_var (distributions.rs:385), the IEEE quotient exactly
+      const T ex = (i < D) ? div_by_const(-(d * d), two_var, inv_two_var) : (T)0;
       qpart = (e == 0) ? ex : qpart + ex;
     }
     const T logq = group_sum<LPC>(qpart) + qconst;
     const T lp1 = tg.template eval<LPC, E, true>(y, gdummy, lane);
     const T log_alpha = (lp1 + logq) - (lp + logq);
-    const T lnu = glog_unif(ucache.get(a.seed, ucid, st, TAG_MH_ACC, 0u));
+    T lnu;
+    if constexpr (LPC == 64) {
+      // the accept log-uniforms of a whole draw block in one VALU pass: lane
+      // k evaluates ln u_k of the block (wave-uniform inputs), the step reads
+      // lane st % S back as a scalar (the HMC draw block's form)
+      constexpr int S = Blk<T>::S;
+      const uint64_t b = st / S;
+      if (b != lblk) {
+        T us[S];
+        uniforms_of(draw_block(a.seed, ucid, b, TAG_MH_ACC, 0u), us);
+        T um = us[0];
+#pragma unroll
+        for (int k = 1; k < S; ++k) um = ((lane & (S - 1)) == k) ? us[k] : um;
+        lnl = glog_unif(um);
+        lblk = b;
+      }
+      lnu = lane_k(lnl, (int)(st % S));
+    } else {
+      lnu = glog_unif(ucache.get(a.seed, ucid, st, TAG_MH_ACC, 0u));
+    }
     if (log_alpha > lnu) {
 #pragma unroll
       for (int e = 0; e < E; ++e) x[e] = y[e];

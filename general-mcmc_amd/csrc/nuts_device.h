@@ -30,6 +30,8 @@ template <class T, int E, int K = 2> struct MassDev {
   int kind_ = 0;            // 0 identity, 1 diagonal, 2 dense
   T inv[E], sq[E];          // diagonal
   const T* minvT = nullptr;  // dense M^-1, transposed: minvT[j][i] = M^-1_ij (nuts_run)
+  int minv_lds = 0;          // minvT copied to LDS: the chain's slot at byte offset lds_off
+  unsigned lds_off = 0;
   const T* cholT = nullptr;  // its Cholesky factor L, transposed: cholT[j][i] = L_ij
   int D = 0;
   __device__ __forceinline__ int kind() const {
@@ -37,6 +39,13 @@ template <class T, int E, int K = 2> struct MassDev {
     else return 0;
   }
 };
+
+// columns per batch of the dense products (their loads / broadcasts issued
+// together; the sums stay in ascending j). 4 keeps the dense-metric kernel
+// within 256 registers (2 waves per SIMD; 8 took it to 276 and 1 wave).
+#ifndef GM_DENSE_BATCH
+#define GM_DENSE_BATCH 4
+#endif
 
 // inv_mul (:255-273): v = M^-1 p
 template <int LPC, int E, class T, int K>
@@ -51,20 +60,26 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E, K>& M, const T (&p)[
     // columns in batches of 8: a batch's loads and broadcasts are issued
     // together (a runtime-trip loop around the shuffles is not unrolled by the
     // compiler); the sums stay in ascending j
-    for (int j0 = 0; j0 < M.D; j0 += 8) {
-      T mv[8][E], pv[8];
+    constexpr int GB = GM_DENSE_BATCH;
+    for (int j0 = 0; j0 < M.D; j0 += GB) {
+      T mv[GB][E], pv[GB];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < GB; ++u) {
         const int j = (j0 + u < M.D) ? j0 + u : M.D - 1;
         pv[u] = coord<LPC, E>(p, j);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           const int i = lane * E + e;
-          mv[u][e] = (i < M.D) ? M.minvT[(long long)j * M.D + i] : (T)0;  // a chain's lanes: one row
+          // a chain's lanes: one row; from the LDS copy when present (the
+          // address is formed from the LDS base so that it is a ds_read)
+          if (M.minv_lds)
+            mv[u][e] = (i < M.D) ? ((const T*)(gm_dyn_lds + M.lds_off))[j * M.D + i] : (T)0;
+          else
+            mv[u][e] = (i < M.D) ? M.minvT[(long long)j * M.D + i] : (T)0;
         }
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < GB; ++u) {
         if (j0 + u < M.D) {
 #pragma unroll
           for (int e = 0; e < E; ++e)
@@ -90,10 +105,11 @@ __device__ __forceinline__ void momentum_from(const MassDev<T, E, K>& M, const T
     T acc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
-    for (int j0 = 0; j0 < M.D; j0 += 8) {  // batches of 8 columns, as inv_mul
-      T mv[8][E], zv[8];
+    constexpr int GB = GM_DENSE_BATCH;
+    for (int j0 = 0; j0 < M.D; j0 += GB) {  // batches of GB columns, as inv_mul
+      T mv[GB][E], zv[GB];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < GB; ++u) {
         const int j = (j0 + u < M.D) ? j0 + u : M.D - 1;
         zv[u] = coord<LPC, E>(z, j);
 #pragma unroll
@@ -103,7 +119,7 @@ __device__ __forceinline__ void momentum_from(const MassDev<T, E, K>& M, const T
         }
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < GB; ++u) {
         const int j = j0 + u;
         if (j < M.D) {
 #pragma unroll
@@ -342,7 +358,7 @@ __device__ unsigned long long gm_nuts_prof_buf[NPROF_WAVES * NPROF_SLOTS];
 #endif
 
 template <class T, int LPC, int E, class TG, int MASS>
-__global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
+__global__ __launch_bounds__(256, 2) void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
   const int lane = (int)(gtid % LPC);
@@ -452,6 +468,21 @@ __global__ __launch_bounds__(256) void nuts_kernel(NutsLaunch a, TG tg_) {
     if (MASS == 2 && a.mass_mode == 2) {
       M.minvT = (const T*)a.minv + (long long)c * D * D;
       M.cholT = (const T*)a.mchol + (long long)c * D * D;
+      if (a.minv_lds) {
+        // the chain's M^-1 into its LDS slot: every lane copies exactly the
+        // entries it reads in inv_mul (column j of its coordinates i, for
+        // every j), so no lane reads another lane's writes (no barrier)
+        M.lds_off = a.minv_lds_off + (unsigned)((threadIdx.x / LPC) * D * D * sizeof(T));
+        T* ml = (T*)(gm_dyn_lds + M.lds_off);
+        for (int jj = 0; jj < D; ++jj) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const int i = lane * E + e;
+            if (i < D) ml[jj * D + i] = M.minvT[(long long)jj * D + i];
+          }
+        }
+        M.minv_lds = 1;
+      }
     }
     rn = a.rn[c];
   }

@@ -1,3 +1,4 @@
+#include <cstdlib>
 // nuts_kernels.hip — many-chain No-U-Turn sampler for gfx950.
 //
 // Restates GenericNUTSChain::step (generic_nuts.rs:755-925) with the identity
@@ -397,6 +398,10 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
   uint64_t refind_step = 0;
   NutsLdsBudget budget;
   budget.lds_cap = ns.lds_levels_cap;  // gm_nuts_set_lds_levels (-1: as many as fit)
+  {
+    const char* e = std::getenv("GMCMC_NUTS_MINV_LDS");  // A/B switch; identical results
+    budget.minv_lds = (e && e[0] == '0') ? 0 : 1;
+  }
   {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||

@@ -17,6 +17,7 @@ struct NutsLdsBudget {
   int ncu = 256;                // compute units
   int lds_max = 64 * 1024;      // dynamic LDS per block
   long long lds_cap = -1;       // levels cap (-1: as many as fit)
+  int minv_lds = 1;             // dense metric in LDS when it fits (GMCMC_NUTS_MINV_LDS=0: off)
 };
 
 // LDS of a launch: the target's staging area (tgl bytes), then as many
@@ -31,6 +32,22 @@ inline size_t nuts_size_lds(NutsLaunch& a, const NutsLdsBudget& b, unsigned bloc
   bpc = bpc < 1 ? 1 : bpc > 4 ? 4 : bpc;
   size_t budget = (size_t)(160 * 1024) / (size_t)bpc - 1024;
   if (budget > (size_t)b.lds_max) budget = (size_t)b.lds_max;
+  // Dense metric: the block's chains' M^-1 (D*D each) in LDS when it fits a
+  // block of its own (one block per CU: the per-chain matrices otherwise
+  // stream from L2/MALL at every drift and kinetic energy, 2 x D*D*s bytes
+  // per leapfrog)
+  a.minv_lds = 0;
+  a.minv_lds_off = 0;
+  if (a.mass_mode == 2 && b.minv_lds) {
+    const size_t mb = (size_t)(256 / LPC) * a.D * a.D * tsz;
+    const size_t lim = (size_t)b.lds_max < (size_t)(160 * 1024) ? (size_t)b.lds_max : (size_t)(160 * 1024);
+    if (tgl + mb <= lim) {
+      a.minv_lds = 1;
+      a.minv_lds_off = (unsigned)tgl;
+      tgl += (mb + 15) / 16 * 16;
+      budget = lim;
+    }
+  }
   long long kl = budget > tgl ? (long long)((budget - tgl) / per_level) : 0;
   if (kl > a.max_depth) kl = a.max_depth;
   if (b.lds_cap >= 0 && kl > b.lds_cap) kl = b.lds_cap;
