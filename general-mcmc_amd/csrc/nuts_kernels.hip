@@ -399,8 +399,12 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
   NutsLdsBudget budget;
   budget.lds_cap = ns.lds_levels_cap;  // gm_nuts_set_lds_levels (-1: as many as fit)
   {
-    const char* e = std::getenv("GMCMC_NUTS_MINV_LDS");  // A/B switch; identical results
-    budget.minv_lds = (e && e[0] == '0') ? 0 : 1;
+    // M^-1 in LDS takes a CU's LDS for one block (1 wave per SIMD): measured
+    // slower (1.85e8 vs 2.35e8 leapfrogs/s, cfg3 dense) than re-reading it from
+    // L2/MALL at 2 waves per SIMD, so off unless GMCMC_NUTS_MINV_LDS=1 (an
+    // A/B switch; identical results)
+    const char* e = std::getenv("GMCMC_NUTS_MINV_LDS");
+    budget.minv_lds = (e && e[0] == '1') ? 1 : 0;
   }
   {
     int dev = 0;

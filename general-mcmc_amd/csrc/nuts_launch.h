@@ -17,7 +17,7 @@ struct NutsLdsBudget {
   int ncu = 256;                // compute units
   int lds_max = 64 * 1024;      // dynamic LDS per block
   long long lds_cap = -1;       // levels cap (-1: as many as fit)
-  int minv_lds = 1;             // dense metric in LDS when it fits (GMCMC_NUTS_MINV_LDS=0: off)
+  int minv_lds = 0;             // dense metric in LDS when it fits (GMCMC_NUTS_MINV_LDS=1: on)
 };
 
 // LDS of a launch: the target's staging area (tgl bytes), then as many

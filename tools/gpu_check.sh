@@ -30,7 +30,8 @@ for step in "$@"; do
     nlevels) run nuts_levels 300 python tools/probe_nuts_levels.py ;;
     masstest) run mass_tests 300 python -u -m pytest tests/test_gpu_nuts_mass.py tests/test_gpu_mfma_gauss.py tests/test_gpu_nuts_truncation.py -x -q --timeout 120 --timeout-method thread ;;
     densemass) run dense_lds0 300 env GMCMC_NUTS_MINV_LDS=0 python tools/bench_configs.py --which 3 --nuts-mass dense &&
-               run dense_lds1 300 env GMCMC_NUTS_MINV_LDS=1 python tools/bench_configs.py --which 3 --nuts-mass dense ;;
+               run dense_lds1 300 env GMCMC_NUTS_MINV_LDS=1 python tools/bench_configs.py --which 3 --nuts-mass dense &&
+               run dense_lds1_test 300 env GMCMC_NUTS_MINV_LDS=1 python -u -m pytest tests/test_gpu_nuts_mass.py -x -q --timeout 120 --timeout-method thread ;;
     mhtest) run mh_tests 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize_edge.py tests/test_gpu_tracker.py -x -q -k "mh or MH or cfg5 or Metropolis or tracker" --timeout 120 --timeout-method thread ;;
     warmup) run warmup_probe 300 python tools/probe_warmup.py ;;
     hostpath) run host_path 120 python tools/probe_host_path.py ;;
