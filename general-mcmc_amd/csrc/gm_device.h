@@ -486,18 +486,21 @@ template <class T> struct IsoGaussT {
 //
 // Matrix-core form (f64, 16 lanes x 2 coordinates per chain, D <= 32: NUTS
 // cfg3's layout). A wave holds 4 chains; w = P [d_0 .. d_3] is a 32x32 by
-// 32x4 product, 16 v_mfma_f64_4x4x4_4b_f64 (two 16-row halves g x eight
-// 4-column steps s; the 4 blocks of an instruction are the 4 row tiles of a
-// half, the 4 columns of a block are the wave's 4 chains). Measured on gfx950
-// (tools/probes/mfma_f64_probe.hip, profiles/r02/mfma/): the instruction's
-// result is bit for bit the k-ascending fma chain from C, so accumulating s
-// ascending from C = +0 is exactly the oracle's j-ascending chain; lane
-// l = 16r + 4b + q holds A[m=q][k=r], B[k=r][n=q] and C/D[m=r][n=q] of block
-// b. bind() stages P once per block in fragment order (lane l's 16 A values
-// as 8 16-byte pairs); an evaluation publishes d transposed (slot [r][s] =
-// d_{4s+r}, so a lane's 8 B values are 64 contiguous bytes), issues the 16
-// instructions, and routes w back to the chains' lanes through a second
-// slot. All 64 lanes take part, so the form runs only with the whole wave
+// 32x4 product, 16 v_mfma_f64_4x4x4_4b_f64 (two output halves g x eight
+// 4-column steps s). Measured on gfx950 (tools/probes/mfma_f64_probe.hip,
+// profiles/r02/mfma/): the instruction's result is bit for bit the
+// k-ascending fma chain from C, so accumulating s ascending from C = +0 is
+// exactly the oracle's j-ascending chain (a product's two factors commute);
+// lane l = 16r + 4b + q holds A[m=q][k=r], B[k=r][n=q] and C/D[m=r][n=q] of
+// block b. The chains are the rows of the product: A = the 4 chains' d
+// (A[m][k] = d_m[4s + k]) and B = P^T (B[k][n] of block b = P[8b + 2n + g]
+// [4s + k]), so C/D[m][n] of block b lands on lane 16m + 4b + n, i.e. on
+// chain m's own lane 4b + n as its coordinate 2(4b + n) + g = w[e = g]: the
+// result needs no routing. A lane's A values are the d of chain l&3 at
+// 4s + (l>>4), s = 0..7, read from a per-chain LDS slot where d is published
+// transposed (slot [r][s] = d_{4s+r}: 64 contiguous bytes per lane). bind()
+// stages B once per block in fragment order (lane l's 16 values as 8 16-byte
+// pairs). All 64 lanes take part, so the form runs only with the whole wave
 // active (a partial last wave, or a chain-divergent call such as the step
 // size search, takes the global-memory VALU product: the same chain, so the
 // same bits).
@@ -524,7 +527,7 @@ template <class T> struct GaussT {
   }
   // dynamic LDS bytes a 256-thread block needs for layout (LPC, E)
   template <int LPC, int E> __host__ __device__ static size_t lds_need(int D) {
-    if (mfma_form<LPC, E>() && D <= 32) return ((size_t)1024 + (size_t)2 * (256 / LPC) * GM_MF_SLOT) * sizeof(T);
+    if (mfma_form<LPC, E>() && D <= 32) return ((size_t)1024 + (size_t)(256 / LPC) * GM_MF_SLOT) * sizeof(T);
     return ((size_t)D * LPC * E + (size_t)256 * E) * sizeof(T);
   }
   template <int LPC, int E> __host__ __device__ size_t lds_bytes() const {
@@ -542,11 +545,11 @@ template <class T> struct GaussT {
     r.sd = nullptr;
     r.mf = false;
     if constexpr (mfma_form<LPC, E>()) {
-      if (use_lds && D <= 32) {  // fragment order: k = (pair * 64 + lane) * 2 + (f & 1), f = 8g + s
+      if (use_lds && D <= 32) {  // fragment order: k = (s * 64 + lane) * 2 + g
         T* sp = (T*)gm_dyn_lds;
         for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
-          const int l = (k >> 1) & 63, f = ((k >> 7) << 1) | (k & 1);
-          const int row = 16 * (f >> 3) + 4 * ((l >> 2) & 3) + (l & 3), col = 4 * (f & 7) + (l >> 4);
+          const int l = (k >> 1) & 63, g = k & 1, st = k >> 7;
+          const int row = 8 * ((l >> 2) & 3) + 2 * (l & 3) + g, col = 4 * st + (l >> 4);
           sp[k] = (row < D && col < D) ? prec[(long long)col * D + row] : (T)0;
         }
         __syncthreads();
@@ -617,31 +620,23 @@ template <class T, int LPC, int E> struct GaussLane {
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // B: chain l&3's d_{4s + (l>>4)}, s = 0..7
-      const T* bt = sprec + 1024 + (wb + (l & 3)) * GM_MF_SLOT + (l >> 4) * 8;
-      v2 bv[4], av[8];
+      // A: chain l&3's d_{4s + (l>>4)}, s = 0..7
+      const T* at = sprec + 1024 + (wb + (l & 3)) * GM_MF_SLOT + (l >> 4) * 8;
+      v2 dv[4], pv[8];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) bv[t] = *(const v2*)(bt + 2 * t);
+      for (int t = 0; t < 4; ++t) dv[t] = *(const v2*)(at + 2 * t);
 #pragma unroll
-      for (int t = 0; t < 8; ++t) av[t] = *(const v2*)(sprec + (t * 64 + l) * 2);
-      double acc0 = 0.0, acc1 = 0.0;  // rows 4b + (l>>4) of the halves g = 0, 1
+      for (int t = 0; t < 8; ++t) pv[t] = *(const v2*)(sprec + (t * 64 + l) * 2);
+      // D[m = l>>4][n = l&3] of block (l>>2)&3: chain l>>4's w at 2(l&15) + g, this lane's w[g]
+      double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
-        const double b = bv[s >> 1][s & 1];
-        acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(av[s >> 1][s & 1], b, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(av[4 + (s >> 1)][s & 1], b, acc1, 0, 0, 0);
+        const double a = dv[s >> 1][s & 1];
+        acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, pv[s][0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, pv[s][1], acc1, 0, 0, 0);
       }
-      // D[m = l>>4][n = l&3] of block (l>>2)&3: chain l&3's w at row 4((l>>2)&3) + (l>>4) (+16)
-      T* ws = const_cast<T*>(sprec) + 1024 + 16 * GM_MF_SLOT;  // after the 16 d slots of the block
-      const int row = 4 * ((l >> 2) & 3) + (l >> 4);
-      ws[(wb + (l & 3)) * GM_MF_SLOT + row] = acc0;
-      ws[(wb + (l & 3)) * GM_MF_SLOT + 16 + row] = acc1;
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const v2 wv = *(const v2*)(ws + (threadIdx.x >> 4) * GM_MF_SLOT + (l & 15) * E);
-      w[0] = wv[0];
-      w[1] = wv[1];
+      w[0] = acc0;
+      w[1] = acc1;
 #ifdef GM_NUTS_PROF
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the product's last read has landed
       prof_prod += __builtin_amdgcn_s_memtime() - pt0;

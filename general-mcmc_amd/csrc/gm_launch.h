@@ -101,12 +101,16 @@ struct NutsLaunch {
   // target's staging area, at byte offset lds_stack_off), the rest in HBM
   int lds_levels = 0;
   unsigned lds_stack_off = 0;
-  // dense metric (mass_mode 2): each chain's transposed M^-1 copied into LDS
-  // at kernel start (D*D elements per chain of the block, at byte offset
+  // dense metric (mass_mode 2): each chain's M^-1 copied into LDS at kernel
+  // start as its packed lower triangle (layout 16 x 2, at byte offset
   // minv_lds_off) when minv_lds, instead of re-read from L2/MALL at every
-  // product (nuts_size_lds decides; nuts_device.h)
+  // product (nuts_size_lds decides; nuts_device.h minv_packed_lds)
   int minv_lds = 0;
   unsigned minv_lds_off = 0;
+  // and its Cholesky factor (the momentum draws), packed the same way, when
+  // chol_lds (after M^-1, before the stack levels)
+  int chol_lds = 0;
+  unsigned chol_lds_off = 0;
   long long sb = 0, eb = 0;  // start_buffer, end_buffer (should_collect, :153-162)
   int do_refind = 0;         // re-find eps for updated chains first (:905-918)
   uint64_t refind_step = 0;  // transition index of the update (probe draws)

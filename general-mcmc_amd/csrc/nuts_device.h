@@ -30,15 +30,100 @@ template <class T, int E, int K = 2> struct MassDev {
   int kind_ = 0;            // 0 identity, 1 diagonal, 2 dense
   T inv[E], sq[E];          // diagonal
   const T* minvT = nullptr;  // dense M^-1, transposed: minvT[j][i] = M^-1_ij (nuts_run)
-  int minv_lds = 0;          // minvT copied to LDS: the chain's slot at byte offset lds_off
+  int minv_lds = 0;          // M^-1 resident in LDS, packed (minv_packed_lds): the chain's slot at lds_off
   unsigned lds_off = 0;
   const T* cholT = nullptr;  // its Cholesky factor L, transposed: cholT[j][i] = L_ij
+  int chol_lds = 0;          // L resident in LDS, rows packed: the chain's slot at chol_off
+  unsigned chol_off = 0;
   int D = 0;
   __device__ __forceinline__ int kind() const {
     if constexpr (K > 0) return kind_;
     else return 0;
   }
 };
+
+// Dense M^-1 resident in LDS (layout 16 x 2, the matrix-core layout of cfg3).
+// M^-1 is exactly symmetric (invert_spd_from_cholesky writes inv[i][j] and
+// inv[j][i] from one sum), so a chain keeps only its lower triangle, rows
+// packed: M^-1_ij at tri(max(i,j)) + min(i,j), tri(i) = i(i+1)/2, over the
+// DP = LPC*E padded rows (zeros past D): 528 doubles = 4,224 B per chain at
+// D = 32, so the 16 chains of a block take 67,584 B and two blocks per CU
+// (2 waves per SIMD) still fit the 160 KiB next to the target's staging (the
+// full matrices, 128 KiB per block, allowed one block per CU only and ran
+// slower than re-reading them from L2/MALL). A lane's row r reads, for
+// column j, tri(r) + j while j <= r and tri(j) + r after: one address select
+// per element, its immediate offset 8j common to both forms. p_j reaches the
+// chain's lanes by a DPP row broadcast (row_newbcast: a chain is one 16-lane
+// DPP row), no LDS traffic. The sums are the global form's (j ascending from
+// +0, separate multiply and add), so the bits are the oracle's.
+__host__ __device__ constexpr int tri_n(int i) { return i * (i + 1) / 2; }
+template <int LPC, int E, class T> __host__ __device__ constexpr size_t minv_packed_bytes() {
+  return (size_t)tri_n(LPC * E) * sizeof(T);
+}
+template <int K> __device__ __forceinline__ double row_bcast(double v) {  // lane K of the 16-lane row
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, 0x150 + K, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), 0x150 + K, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+template <int K> __device__ __forceinline__ float row_bcast(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x150 + K, 0xf, 0xf,
+                                                               false));
+}
+// coordinates J+K .. J+NB-1 of a 16-lane chain's vector (E per lane) into
+// pj[K ..], each broadcast to the chain's lanes
+template <int E, class T, int J, int K, int NB>
+__device__ __forceinline__ void row_bcasts(const T (&p)[E], T (&pj)[NB]) {
+  if constexpr (K < NB) {
+    pj[K] = row_bcast<(J + K) / E>(p[(J + K) % E]);
+    row_bcasts<E, T, J, K + 1, NB>(p, pj);
+  }
+}
+// Columns [J, J + NB) of v = M^-1 p from the packed triangle: the batch's
+// LDS reads and row broadcasts are issued first (a straight-line stretch the
+// scheduler cannot reorder past the sched_barrier), then its sums in
+// ascending j. No test j < D: the padded coordinates of p and the padded
+// rows/columns of the triangle are exactly +0, and adding +0 leaves an
+// accumulator that starts at +0 unchanged (it can never become -0: x + y
+// rounds to -0 only when both are -0), so the padded columns change no bit.
+#ifndef GM_PACKED_BATCH
+#define GM_PACKED_BATCH 16
+#endif
+template <int LPC, int E, class T, int J, bool CHOL>
+__device__ __forceinline__ void packed_cols(const unsigned (&aA)[E], const unsigned (&aB)[E], const int (&r)[E],
+                                            const T (&p)[E], T (&acc)[E]) {
+  constexpr int NB = GM_PACKED_BATCH < LPC * E - J ? GM_PACKED_BATCH : LPC * E - J;
+  if constexpr (NB > 0) {
+    T m[NB][E], pj[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int j = J + u;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        unsigned ad;
+        if constexpr (CHOL)  // L: row r's entries j <= r are contiguous; j > r is +-0 (below)
+          ad = aA[e] + (unsigned)(((j <= r[e]) ? j : 0) * (int)sizeof(T));
+        else  // M^-1: tri(r) + j while j <= r, tri(j) + r after
+          ad = (j <= r[e]) ? aA[e] + (unsigned)(j * (int)sizeof(T))
+                           : aB[e] + (unsigned)(tri_n(j) * (int)sizeof(T));
+        m[u][e] = *(const T*)(gm_dyn_lds + ad);
+      }
+    }
+    row_bcasts<E, T, J, 0, NB>(p, pj);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        // p = L z skips the terms j > r (L_rj = 0); adding 0 * z_j = +-0 to
+        // the +0-started sum changes no bit either
+        const T mm = (CHOL && J + u > r[e]) ? (T)0 : m[u][e];
+        acc[e] = acc[e] + mm * pj[u];
+      }
+    }
+    packed_cols<LPC, E, T, J + NB, CHOL>(aA, aB, r, p, acc);
+  }
+}
 
 // columns per batch of the dense products (their loads / broadcasts issued
 // together; the sums stay in ascending j). 4 keeps the dense-metric kernel
@@ -57,6 +142,22 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E, K>& M, const T (&p)[
     T acc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
+    if constexpr (LPC == 16 && E == 2) {
+      if (M.minv_lds) {
+        unsigned aA[E], aB[E];
+        int r[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          r[e] = lane * E + e;
+          aA[e] = M.lds_off + (unsigned)(tri_n(r[e]) * (int)sizeof(T));
+          aB[e] = M.lds_off + (unsigned)(r[e] * (int)sizeof(T));
+        }
+        packed_cols<LPC, E, T, 0, false>(aA, aB, r, p, acc);
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = acc[e];
+        return;
+      }
+    }
     // columns in batches of 8: a batch's loads and broadcasts are issued
     // together (a runtime-trip loop around the shuffles is not unrolled by the
     // compiler); the sums stay in ascending j
@@ -70,12 +171,7 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E, K>& M, const T (&p)[
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           const int i = lane * E + e;
-          // a chain's lanes: one row; from the LDS copy when present (the
-          // address is formed from the LDS base so that it is a ds_read)
-          if (M.minv_lds)
-            mv[u][e] = (i < M.D) ? ((const T*)(gm_dyn_lds + M.lds_off))[j * M.D + i] : (T)0;
-          else
-            mv[u][e] = (i < M.D) ? M.minvT[(long long)j * M.D + i] : (T)0;
+          mv[u][e] = (i < M.D) ? M.minvT[(long long)j * M.D + i] : (T)0;
         }
       }
 #pragma unroll
@@ -105,6 +201,21 @@ __device__ __forceinline__ void momentum_from(const MassDev<T, E, K>& M, const T
     T acc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
+    if constexpr (LPC == 16 && E == 2) {
+      if (M.chol_lds) {
+        unsigned aA[E];
+        int r[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          r[e] = lane * E + e;
+          aA[e] = M.chol_off + (unsigned)(tri_n(r[e]) * (int)sizeof(T));
+        }
+        packed_cols<LPC, E, T, 0, true>(aA, aA, r, z, acc);
+#pragma unroll
+        for (int e = 0; e < E; ++e) p[e] = acc[e];
+        return;
+      }
+    }
     constexpr int GB = GM_DENSE_BATCH;
     for (int j0 = 0; j0 < M.D; j0 += GB) {  // batches of GB columns, as inv_mul
       T mv[GB][E], zv[GB];
@@ -357,8 +468,11 @@ constexpr int NPROF_WAVES = 8192;
 __device__ unsigned long long gm_nuts_prof_buf[NPROF_WAVES * NPROF_SLOTS];
 #endif
 
+// Launch bound: 2 blocks (2 waves per SIMD) per CU, 256 registers per lane;
+// the dense-metric instantiation 1 (512: at 256 it spilled ~500 B per lane to
+// scratch inside the loop, measured 2.1e8 leapfrogs/s at cfg3).
 template <class T, int LPC, int E, class TG, int MASS>
-__global__ __launch_bounds__(256, 2) void nuts_kernel(NutsLaunch a, TG tg_) {
+__global__ __launch_bounds__(256, MASS == 2 ? 1 : 2) void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
   const int lane = (int)(gtid % LPC);
@@ -468,20 +582,33 @@ __global__ __launch_bounds__(256, 2) void nuts_kernel(NutsLaunch a, TG tg_) {
     if (MASS == 2 && a.mass_mode == 2) {
       M.minvT = (const T*)a.minv + (long long)c * D * D;
       M.cholT = (const T*)a.mchol + (long long)c * D * D;
-      if (a.minv_lds) {
-        // the chain's M^-1 into its LDS slot: every lane copies exactly the
-        // entries it reads in inv_mul (column j of its coordinates i, for
-        // every j), so no lane reads another lane's writes (no barrier)
-        M.lds_off = a.minv_lds_off + (unsigned)((threadIdx.x / LPC) * D * D * sizeof(T));
-        T* ml = (T*)(gm_dyn_lds + M.lds_off);
-        for (int jj = 0; jj < D; ++jj) {
+      if constexpr (LPC == 16 && E == 2) {
+        if (a.minv_lds) {
+          // the chain's M^-1 into its LDS slot, lower triangle packed
+          // (minv_packed_lds): each lane writes its own rows; the chain's
+          // lanes (one wave) read each other's rows after the wave barrier
+          M.lds_off = a.minv_lds_off + (unsigned)(cib * minv_packed_bytes<LPC, E, T>());
+          T* ml = (T*)(gm_dyn_lds + M.lds_off);
 #pragma unroll
           for (int e = 0; e < E; ++e) {
-            const int i = lane * E + e;
-            if (i < D) ml[jj * D + i] = M.minvT[(long long)jj * D + i];
+            const int r = lane * E + e;
+            for (int jj = 0; jj <= r; ++jj) ml[tri_n(r) + jj] = (r < D) ? M.minvT[(long long)jj * D + r] : (T)0;
           }
+          M.minv_lds = 1;
+          if (a.chol_lds) {  // and its Cholesky factor's rows, packed the same way
+            M.chol_off = a.chol_lds_off + (unsigned)(cib * minv_packed_bytes<LPC, E, T>());
+            T* cl = (T*)(gm_dyn_lds + M.chol_off);
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+              const int r = lane * E + e;
+              for (int jj = 0; jj <= r; ++jj) cl[tri_n(r) + jj] = (r < D) ? M.cholT[(long long)jj * D + r] : (T)0;
+            }
+            M.chol_lds = 1;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        M.minv_lds = 1;
       }
     }
     rn = a.rn[c];

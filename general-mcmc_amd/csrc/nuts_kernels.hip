@@ -1,4 +1,5 @@
 #include <cstdlib>
+#include <cstdio>
 // nuts_kernels.hip — many-chain No-U-Turn sampler for gfx950.
 //
 // Restates GenericNUTSChain::step (generic_nuts.rs:755-925) with the identity
@@ -399,12 +400,13 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
   NutsLdsBudget budget;
   budget.lds_cap = ns.lds_levels_cap;  // gm_nuts_set_lds_levels (-1: as many as fit)
   {
-    // M^-1 in LDS takes a CU's LDS for one block (1 wave per SIMD): measured
-    // slower (1.85e8 vs 2.35e8 leapfrogs/s, cfg3 dense) than re-reading it from
-    // L2/MALL at 2 waves per SIMD, so off unless GMCMC_NUTS_MINV_LDS=1 (an
-    // A/B switch; identical results)
+    // dense M^-1 resident in LDS (packed lower triangles, layout 16 x 2) when
+    // it fits; GMCMC_NUTS_MINV_LDS=0 keeps it in global memory (an A/B
+    // switch; identical results)
     const char* e = std::getenv("GMCMC_NUTS_MINV_LDS");
-    budget.minv_lds = (e && e[0] == '1') ? 1 : 0;
+    budget.minv_lds = (e && e[0] == '0') ? 0 : 1;
+    const char* e2 = std::getenv("GMCMC_NUTS_CHOL_LDS");
+    budget.chol_lds = (e2 && e2[0] == '0') ? 0 : 1;
   }
   {
     int dev = 0;
@@ -497,6 +499,15 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
       e = jit_launch(JIT_NUTS, dt, tg, blocks, 256, lds, st, args);
     } else {
       e = nuts_launch_layout(dt, tg, lay, a, st, budget);
+    }
+    {
+      static const bool dbg = [] {  // GMCMC_NUTS_DEBUG=1: the LDS plan of each launch on stderr
+        const char* v = std::getenv("GMCMC_NUTS_DEBUG");
+        return v && v[0] == '1';
+      }();
+      if (dbg)
+        fprintf(stderr, "gmcmc nuts launch: lds_max %d ncu %d stack levels in LDS %d, M^-1 in LDS %d at %u, L %d at %u\n",
+                budget.lds_max, budget.ncu, a.lds_levels, a.minv_lds, a.minv_lds_off, a.chol_lds, a.chol_lds_off);
     }
     if (e != hipSuccess) {
       set_error(std::string("NUTS launch failed: ") + hipGetErrorString(e));

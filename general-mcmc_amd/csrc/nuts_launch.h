@@ -17,7 +17,8 @@ struct NutsLdsBudget {
   int ncu = 256;                // compute units
   int lds_max = 64 * 1024;      // dynamic LDS per block
   long long lds_cap = -1;       // levels cap (-1: as many as fit)
-  int minv_lds = 0;             // dense metric in LDS when it fits (GMCMC_NUTS_MINV_LDS=1: on)
+  int minv_lds = 1;             // dense metric in LDS when it fits (GMCMC_NUTS_MINV_LDS=0: off)
+  int chol_lds = 1;             // its Cholesky factor too (GMCMC_NUTS_CHOL_LDS=0: off)
 };
 
 // LDS of a launch: the target's staging area (tgl bytes), then as many
@@ -30,22 +31,33 @@ inline size_t nuts_size_lds(NutsLaunch& a, const NutsLdsBudget& b, unsigned bloc
   const size_t per_level = (size_t)3 * 256 * E * tsz + (size_t)(256 / LPC) * (tsz + 8);
   long long bpc = ((long long)blocks + b.ncu - 1) / b.ncu;
   bpc = bpc < 1 ? 1 : bpc > 4 ? 4 : bpc;
+  // the dense-metric kernel runs one wave per SIMD (its launch bound: 512
+  // registers per lane, the metric's products and state without scratch
+  // spills), so one block per CU holds the CU's LDS
+  if (a.mass_mode == 2) bpc = 1;
   size_t budget = (size_t)(160 * 1024) / (size_t)bpc - 1024;
   if (budget > (size_t)b.lds_max) budget = (size_t)b.lds_max;
-  // Dense metric: the block's chains' M^-1 (D*D each) in LDS when it fits a
-  // block of its own (one block per CU: the per-chain matrices otherwise
-  // stream from L2/MALL at every drift and kinetic energy, 2 x D*D*s bytes
-  // per leapfrog)
+  // Dense metric (layout 16 x 2): the block's chains' M^-1 resident in LDS,
+  // lower triangles packed (nuts_device.h, minv_packed_lds), when it fits
+  // next to the target's staging at the grid's blocks per CU; otherwise the
+  // per-chain matrices stream from L2/MALL at every drift and kinetic energy
+  // (2 x D*D*s bytes per leapfrog)
   a.minv_lds = 0;
   a.minv_lds_off = 0;
-  if (a.mass_mode == 2 && b.minv_lds) {
-    const size_t mb = (size_t)(256 / LPC) * a.D * a.D * tsz;
-    const size_t lim = (size_t)b.lds_max < (size_t)(160 * 1024) ? (size_t)b.lds_max : (size_t)(160 * 1024);
-    if (tgl + mb <= lim) {
+  a.chol_lds = 0;
+  a.chol_lds_off = 0;
+  if (a.mass_mode == 2 && b.minv_lds && LPC == 16 && E == 2 && a.D <= LPC * E) {
+    const size_t dp = (size_t)LPC * E;
+    const size_t mb = (size_t)(256 / LPC) * (dp * (dp + 1) / 2) * tsz;
+    if (tgl + mb <= budget) {
       a.minv_lds = 1;
       a.minv_lds_off = (unsigned)tgl;
       tgl += (mb + 15) / 16 * 16;
-      budget = lim;
+      if (b.chol_lds && tgl + mb <= budget) {
+        a.chol_lds = 1;
+        a.chol_lds_off = (unsigned)tgl;
+        tgl += (mb + 15) / 16 * 16;
+      }
     }
   }
   long long kl = budget > tgl ? (long long)((budget - tgl) / per_level) : 0;

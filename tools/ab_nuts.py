@@ -1,6 +1,6 @@
 """A/B of NUTS cfg3 throughput for libgmcmc variants (GMCMC_LIB), alternating
 processes in one GPU call:  python tools/ab_nuts.py A.so B.so ...
-(variants from tools/ab_build_nuts.sh)."""
+(variants from tools/ab_build_unit.sh)."""
 import json
 import os
 import subprocess
@@ -15,7 +15,7 @@ res = {l: [] for l in libs}
 for r in range(rounds):
     for l in libs:
         env = dict(os.environ, GMCMC_LIB=os.path.abspath(l))
-        out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_configs.py"), "--which", "3"],
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_configs.py"), "--which", "3"] + os.environ.get("AB_ARGS", "").split(),
                              env=env, capture_output=True, text=True, timeout=300)
         if out.returncode:
             print(out.stderr[-2000:])

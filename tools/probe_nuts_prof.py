@@ -29,6 +29,9 @@ def main():
     s = gm.NUTS(dense_gauss_32(), gm.init_det(chains, 32), 0.8, dtype=np.float64, max_depth=10).set_seed(42)
     if layout:
         s.set_layout(*[int(v) for v in layout.split("x")])
+    mass = os.environ.get("MASS", "none")  # diagonal / dense: warm-up metric adaptation
+    if mass != "none":
+        s.set_mass_adaptation(gm.NUTSMassMatrixConfig(mass))
     s.run_positions(1, 200)  # warm-up, step sizes adapted
     lf0 = s.leapfrog_counts().sum()
     s.run_positions(200, 0)
