@@ -30,7 +30,7 @@ template <class T, int E, int K = 2> struct MassDev {
   int kind_ = 0;            // 0 identity, 1 diagonal, 2 dense
   T inv[E], sq[E];          // diagonal
   const T* minvT = nullptr;  // dense M^-1, transposed: minvT[j][i] = M^-1_ij (nuts_run)
-  int minv_lds = 0;          // M^-1 resident in LDS, packed (minv_packed_lds): the chain's slot at lds_off
+  int minv_lds = 0;          // M^-1 resident in LDS: 1 packed (minv_packed_lds), 2 full; the chain's slot at lds_off
   unsigned lds_off = 0;
   const T* cholT = nullptr;  // its Cholesky factor L, transposed: cholT[j][i] = L_ij
   int chol_lds = 0;          // L resident in LDS, rows packed: the chain's slot at chol_off
@@ -125,6 +125,31 @@ __device__ __forceinline__ void packed_cols(const unsigned (&aA)[E], const unsig
   }
 }
 
+// Columns [J, J + NB) of v = M^-1 p from the full matrix in LDS (minv_lds
+// == 2, the one-block-per-CU budget: 8 KiB per chain at D = 32), stored
+// [j][i] so that a lane's two entries of column j are one 16-byte read at an
+// immediate offset: no address arithmetic. Same sums and +0 padding as above.
+template <int LPC, int E, class T, int J>
+__device__ __forceinline__ void full_cols(unsigned base, const T (&p)[E], T (&acc)[E]) {
+  constexpr int DP = LPC * E;
+  constexpr int NB = GM_PACKED_BATCH < DP - J ? GM_PACKED_BATCH : DP - J;
+  if constexpr (NB > 0) {
+    typedef T vE __attribute__((ext_vector_type(E)));
+    vE m[NB];
+    T pj[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) m[u] = *(const vE*)(gm_dyn_lds + base + (J + u) * DP * sizeof(T));
+    row_bcasts<E, T, J, 0, NB>(p, pj);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] = acc[e] + m[u][e] * pj[u];
+    }
+    full_cols<LPC, E, T, J + NB>(base, p, acc);
+  }
+}
+
 // columns per batch of the dense products (their loads / broadcasts issued
 // together; the sums stay in ascending j). 4 keeps the dense-metric kernel
 // within 256 registers (2 waves per SIMD; 8 took it to 276 and 1 wave).
@@ -143,6 +168,12 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E, K>& M, const T (&p)[
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
     if constexpr (LPC == 16 && E == 2) {
+      if (M.minv_lds == 2) {
+        full_cols<LPC, E, T, 0>(M.lds_off + (unsigned)(lane * E * (int)sizeof(T)), p, acc);
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = acc[e];
+        return;
+      }
       if (M.minv_lds) {
         unsigned aA[E], aB[E];
         int r[E];
@@ -583,7 +614,21 @@ __global__ __launch_bounds__(256, MASS == 2 ? 1 : 2) void nuts_kernel(NutsLaunch
       M.minvT = (const T*)a.minv + (long long)c * D * D;
       M.cholT = (const T*)a.mchol + (long long)c * D * D;
       if constexpr (LPC == 16 && E == 2) {
-        if (a.minv_lds) {
+        if (a.minv_lds == 2) {
+          // the chain's M^-1 into its LDS slot, full and transposed ([j][i]):
+          // each lane copies exactly the entries it reads (no barrier)
+          constexpr int DP = LPC * E;
+          M.lds_off = a.minv_lds_off + (unsigned)(cib * DP * DP * sizeof(T));
+          T* ml = (T*)(gm_dyn_lds + M.lds_off);
+          for (int jj = 0; jj < DP; ++jj) {
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+              const int r = lane * E + e;
+              ml[jj * DP + r] = (r < D && jj < D) ? M.minvT[(long long)jj * D + r] : (T)0;
+            }
+          }
+          M.minv_lds = 2;
+        } else if (a.minv_lds) {
           // the chain's M^-1 into its LDS slot, lower triangle packed
           // (minv_packed_lds): each lane writes its own rows; the chain's
           // lanes (one wave) read each other's rows after the wave barrier

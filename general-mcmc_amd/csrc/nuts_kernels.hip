@@ -400,11 +400,11 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
   NutsLdsBudget budget;
   budget.lds_cap = ns.lds_levels_cap;  // gm_nuts_set_lds_levels (-1: as many as fit)
   {
-    // dense M^-1 resident in LDS (packed lower triangles, layout 16 x 2) when
-    // it fits; GMCMC_NUTS_MINV_LDS=0 keeps it in global memory (an A/B
-    // switch; identical results)
+    // dense M^-1 resident in LDS (layout 16 x 2) when it fits: full matrices
+    // or packed lower triangles (nuts_size_lds); GMCMC_NUTS_MINV_LDS=1 packed
+    // only, 0 global memory (A/B switches; identical results)
     const char* e = std::getenv("GMCMC_NUTS_MINV_LDS");
-    budget.minv_lds = (e && e[0] == '0') ? 0 : 1;
+    budget.minv_lds = (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : 2;
     const char* e2 = std::getenv("GMCMC_NUTS_CHOL_LDS");
     budget.chol_lds = (e2 && e2[0] == '0') ? 0 : 1;
   }

@@ -17,7 +17,8 @@ struct NutsLdsBudget {
   int ncu = 256;                // compute units
   int lds_max = 64 * 1024;      // dynamic LDS per block
   long long lds_cap = -1;       // levels cap (-1: as many as fit)
-  int minv_lds = 1;             // dense metric in LDS when it fits (GMCMC_NUTS_MINV_LDS=0: off)
+  int minv_lds = 2;             // dense metric in LDS when it fits: 2 full or packed, 1 packed only, 0 off
+                                // (GMCMC_NUTS_MINV_LDS)
   int chol_lds = 1;             // its Cholesky factor too (GMCMC_NUTS_CHOL_LDS=0: off)
 };
 
@@ -49,7 +50,12 @@ inline size_t nuts_size_lds(NutsLaunch& a, const NutsLdsBudget& b, unsigned bloc
   if (a.mass_mode == 2 && b.minv_lds && LPC == 16 && E == 2 && a.D <= LPC * E) {
     const size_t dp = (size_t)LPC * E;
     const size_t mb = (size_t)(256 / LPC) * (dp * (dp + 1) / 2) * tsz;
-    if (tgl + mb <= budget) {
+    const size_t mf = (size_t)(256 / LPC) * dp * dp * tsz;
+    if (b.minv_lds != 1 && tgl + mf <= budget) {  // the full matrices (no address arithmetic)
+      a.minv_lds = 2;
+      a.minv_lds_off = (unsigned)tgl;
+      tgl += (mf + 15) / 16 * 16;
+    } else if (tgl + mb <= budget) {
       a.minv_lds = 1;
       a.minv_lds_off = (unsigned)tgl;
       tgl += (mb + 15) / 16 * 16;

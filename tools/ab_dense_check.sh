@@ -8,7 +8,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_nuts_mass.py tests/test_gpu
 rc=$?; tail -3 gpurun_out/ab_dense_tests.log; [ $rc -ne 0 ] && exit $rc
 AB_ARGS="--nuts-mass dense" AB_ROUNDS=${AB_ROUNDS:-2} timeout -k 10 600 python tools/ab_nuts.py abtest/base/libgmcmc.so general-mcmc_amd/lib/libgmcmc.so > gpurun_out/ab_dense.log 2>&1
 rc=$?; tail -12 gpurun_out/ab_dense.log; [ $rc -ne 0 ] && exit $rc
-for v in 0 1 0 1; do
-  GMCMC_NUTS_DEBUG=1 GMCMC_NUTS_CHOL_LDS=$v timeout -k 10 200 python tools/bench_configs.py --which 3 --nuts-mass dense > gpurun_out/dense_chol$v.log 2>&1 || exit $?
-  echo "chol_lds=$v $(grep -o 'L [01] at [0-9]*' gpurun_out/dense_chol$v.log | tail -1) $(grep -o 'stack levels in LDS [0-9]*' gpurun_out/dense_chol$v.log | tail -1) $(grep -o '"leapfrog_per_s": [0-9.e+]*' gpurun_out/dense_chol$v.log)"
+for v in ${AB_MINV:-1 2 1 2}; do
+  GMCMC_NUTS_DEBUG=1 GMCMC_NUTS_MINV_LDS=$v timeout -k 10 200 python tools/bench_configs.py --which 3 --nuts-mass dense > gpurun_out/dense_minv$v.log 2>&1 || exit $?
+  echo "minv_lds=$v $(grep -o 'M^-1 in LDS [0-9]* at [0-9]*, L [01] at [0-9]*' gpurun_out/dense_minv$v.log | tail -1) $(grep -o 'stack levels in LDS [0-9]*' gpurun_out/dense_minv$v.log | tail -1) $(grep -o '"leapfrog_per_s": [0-9.e+]*' gpurun_out/dense_minv$v.log)"
 done

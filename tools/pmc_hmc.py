@@ -93,9 +93,10 @@ def main():
     }
     if fl:
         f32 = fl.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0)
-        entry["pmc_flops"] = {"fp32": f32, "fma_f32_insts": fl.get("SQ_INSTS_VALU_FMA_F32"),
-                              "fp32_tflops": f32 / dur / 1e12, "fp32_frac": f32 / dur / 157.3e12,
-                              "note": "SQ_INSTS_VALU_FLOPS_FP32 of the launch over its traced duration"}
+        entry["pmc_flops"] = {"fp32_lane_flops": 64 * f32, "fma_f32_insts": fl.get("SQ_INSTS_VALU_FMA_F32"),
+                              "fp32_lane_tflops": 64 * f32 / dur / 1e12, "fp32_lane_frac": 64 * f32 / dur / 157.3e12,
+                              "note": "SQ_INSTS_VALU_FLOPS_FP32 x 64 (a per-wave-instruction counter) of the launch "
+                                      "over its traced duration"}
     d = json.load(open(OUT)) if os.path.exists(OUT) else {}
     e = d.setdefault(a.key, {"by_steps": {}})
     e["by_steps"][str(a.steps)] = entry

@@ -101,10 +101,12 @@ def main():
              "source": f"{base}: trace, fetch, write, sq, grbm, flops passes (rocprofv3, one run each)"}
         if fl:
             f32, f64 = fl.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0), fl.get("SQ_INSTS_VALU_FLOPS_FP64", 0.0)
-            e["pmc_flops"] = {"fp32": f32, "fp64": f64, "fma_f32_insts": fl.get("SQ_INSTS_VALU_FMA_F32"),
+            # the counters count per wave instruction: x 64 gives the lanes' flops
+            e["pmc_flops"] = {"fp32_lane_flops": 64 * f32, "fp64_lane_flops": 64 * f64,
+                              "fma_f32_insts": fl.get("SQ_INSTS_VALU_FMA_F32"),
                               "fma_f64_insts": fl.get("SQ_INSTS_VALU_FMA_F64"),
-                              "fp32_tflops": f32 / dur / 1e12, "fp64_tflops": f64 / dur / 1e12,
-                              "fp32_frac": f32 / dur / FP32, "fp64_frac": f64 / dur / FP64}
+                              "fp32_lane_frac": 64 * f32 / dur / FP32, "fp64_lane_frac": 64 * f64 / dur / FP64,
+                              "note": "SQ_INSTS_VALU_FLOPS_* x 64 (per-wave-instruction counters); VALU only"}
         if w == "cfg3":
             r = json_line(os.path.join(logs, "cfg3_trace.log"), "cfg3")
             D = 32
