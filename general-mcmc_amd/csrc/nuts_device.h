@@ -87,7 +87,7 @@ __device__ __forceinline__ void row_bcasts(const T (&p)[E], T (&pj)[NB]) {
 // accumulator that starts at +0 unchanged (it can never become -0: x + y
 // rounds to -0 only when both are -0), so the padded columns change no bit.
 #ifndef GM_PACKED_BATCH
-#define GM_PACKED_BATCH 16
+#define GM_PACKED_BATCH 8
 #endif
 template <int LPC, int E, class T, int J, bool CHOL>
 __device__ __forceinline__ void packed_cols(const unsigned (&aA)[E], const unsigned (&aB)[E], const int (&r)[E],
@@ -790,12 +790,7 @@ __global__ __launch_bounds__(256, MASS == 2 ? 1 : 2) void nuts_kernel(NutsLaunch
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int i = lane * E + e;
-#ifdef GM_KO_MOM  // measurement build only: a cheap unit-variance draw instead of Box-Muller
-        const uint32_t hh = (cid * 0x9E3779B1u) ^ ((uint32_t)st * 0x85EBCA77u) ^ ((uint32_t)i * 0xC2B2AE3Du);
-        z[e] = (i < D) ? ((T)((hh ^ (hh >> 15)) & 0xffffu) * (T)(1.0 / 65536.0) - (T)0.5) * (T)3.4641016 : (T)0;
-#else
         z[e] = (i < D) ? ncache[e].get(a.seed, cid, st, TAG_NUTS_MOM, (uint32_t)i) : (T)0;
-#endif
       }
       momentum_from<LPC, E>(M, z, p0, lane);
     }
