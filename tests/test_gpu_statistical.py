@@ -110,3 +110,30 @@ def test_hmc_rosenbrock_nd_runs_finite(gm):
     s = gm.HMC(gm.RosenbrockND(), gm.init_det(4, 3, np.float32), 0.032, 10)
     x = s.run(400, 50)
     assert x.shape == (4, 400, 3) and np.all(np.isfinite(x))
+
+
+def test_rosenbrock64_two_basins_in_x0(gm):
+    """Pins DESIGN §3's reading of the bench's R-hat: on RosenbrockND (a=1,
+    b=100, distributions.rs:495-555) at cfg2's settings (64-D f32, eps 0.01,
+    L 50, hmc.rs:763-780) HMC chains settle in the x0 ~ +1 or the x0 ~ -1
+    basin (x1 ~ x0^2 either way) and do not cross within the run, so
+    parameter 0's split-R-hat stays large while the other parameters mix.
+    4096 chains from iid N(0,1) (the bench's init), 4000 discarded + 200 kept."""
+    C, D = 4096, 64
+    x0 = gm.init_with_seed(C, D, 42, np.float64).astype(np.float32)
+    s = gm.HMC(gm.RosenbrockND(), x0, 0.01, 50, dtype=np.float32).set_seed(42)
+    sample = s.run(200, 4000)  # [C, N, D]
+    m0 = sample[:, :, 0].mean(axis=1)
+    m1 = sample[:, :, 1].mean(axis=1)
+    neg, pos = m0 < -0.5, m0 > 0.5
+    assert neg.mean() > 0.01 and pos.mean() > 0.01 and neg.mean() + pos.mean() > 0.95, (neg.mean(), pos.mean())
+    assert (np.abs(m0) < 0.3).mean() < 0.02  # (almost) no chain sits between the basins
+    # x1 ~ x0^2 in both basins
+    assert abs(np.median(m1[neg]) - 1.0) < 0.3 and abs(np.median(m1[pos]) - 1.0) < 0.3
+    # the chains of one basin do not visit the other within the kept draws
+    assert np.all(sample[neg, :, 0].max(axis=1) < 0.5)
+    rhat, _ = gm.split_rhat_mean_ess(sample)
+    # the reference's orientation sqrt(W/V) (stats.rs:452-454): far below 1 for
+    # parameter 0 (between-chain variance from the two basins), near 1 elsewhere
+    assert rhat[0] < 0.5, rhat[0]
+    assert np.median(rhat[2:]) > 0.9, np.median(rhat[2:])
