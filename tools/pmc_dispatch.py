@@ -59,7 +59,12 @@ def counters(d, kernel, grid, ordinal):
             acc[r["Counter_Name"]] += float(r["Counter_Value"])
             meta = {"vgpr_count_column": int(r["VGPR_Count"]), "accum_vgpr_count_column": int(r["Accum_VGPR_Count"]),
                     "sgpr_count_column": int(r["SGPR_Count"]), "lds_block_size": int(r["LDS_Block_Size"]),
-                    "scratch_size": int(r["Scratch_Size"]), "kernel_name": r["Kernel_Name"]}
+                    "scratch_size": int(r["Scratch_Size"]), "kernel_name": r["Kernel_Name"],
+                    # rocprofv3's VGPR_Count is the kernel descriptor's granule count x 4; gfx950
+                    # allocates (arch + accumulation) registers in granules of 8, so the registers a
+                    # lane holds are twice the column (checked against the compiler's NumVgprs +
+                    # NumAgprs: 106 -> 56 MH cfg5, 238 -> 120 NUTS cfg3, 256 + 176 -> 216 dense NUTS)
+                    "vgpr_total_per_lane": 2 * int(r["VGPR_Count"])}
     return acc, meta
 
 
