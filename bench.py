@@ -65,7 +65,7 @@ def parse(argv=None):
     p.add_argument("--no-north-star", dest="north_star", action="store_false",
                    help="skip the north_star 16384-chain shape (timed by default after the bench line's "
                         "measurements)")
-    p.add_argument("--configs", default="cfg3,cfg4,cfg5",
+    p.add_argument("--configs", default="cfg3,cfg3_dense,cfg4,cfg5",
                    help="BASELINE.json config legs timed after the headline (comma list, '' for none)")
     return p.parse_args(argv)
 
@@ -87,6 +87,10 @@ CONFIG_LEGS = {
     # (nuts.rs:214-259) of 500 collected after 500 warm-up transitions
     "cfg3": dict(kind="nuts", chains=8192, dim=32, dtype="f64", n_discard=500, n_collect=500,
                  target_accept=0.8, max_depth=10),
+    # the same with GenericNUTS::new_with_mass_matrix's dense metric adaptation
+    # during the warm-up (generic_nuts.rs:33-359)
+    "cfg3_dense": dict(kind="nuts", chains=8192, dim=32, dtype="f64", n_discard=500, n_collect=500,
+                       target_accept=0.8, max_depth=10, mass="dense"),
     # configs[3]: batched HMC, RosenbrockND 128-D f32, 65,536 chains over 8 GPUs
     "cfg4": dict(kind="hmc", chains=8192, dim=128, dtype="f32", n_discard=100, n_collect=100,
                  eps=0.01, L=50),
@@ -137,16 +141,17 @@ class GpuBench:
         dt = np.float32 if cfg["dtype"] == "f32" else np.float64
         C, D = cfg["chains"], cfg["dim"]
         x0 = gm.init_with_seed(C, D, 42, np.float64, row0=offset).astype(dt)
-        if cfg["kind"] == "nuts":
-            mean, cov = dense_gauss_32()
-            s = gm.NUTS(gm.DenseGaussian(mean, cov), x0, cfg["target_accept"], dtype=dt,
-                        max_depth=cfg["max_depth"], chain_offset=offset).set_seed(42)
-        elif cfg["kind"] == "hmc":
-            s = gm.HMC(gm.RosenbrockND(), x0, cfg["eps"], cfg["L"], dtype=dt, chain_offset=offset).set_seed(42)
-        else:
-            s = gm.MetropolisHastings(gm.IsotropicGaussian(1.0), gm.IsotropicGaussian(cfg["proposal_std"]),
-                                      x0, dtype=dt, chain_offset=offset).seed(42)
+        s = self._same_kind(cfg, dt, x0, offset, 42)
         try:
+            # untimed: one transition of the same kernel on a scratch copy of the
+            # sampler (its own chains and buffers), so that the timed run does
+            # not include the kernel's first-launch cost (code-object load; 3-4
+            # ms on the cfg5 MH leg before this warm-up, profiles/r03/final)
+            w = self._same_kind(cfg, dt, x0, offset, 7)
+            w.set_layout(*s.layout())
+            w.run_positions(1, 0)
+            self.sync()
+            w.close()
             s.reserve(cfg["n_collect"])
             lf0 = int(s.leapfrog_counts().sum())
             self.sync()
@@ -188,6 +193,21 @@ class GpuBench:
         if warm:
             out.update(warm)
         return out
+
+    def _same_kind(self, cfg, dt, x0, offset, seed):
+        """A sampler of the config's kind, dtype and shape (BASELINE.json configs)."""
+        gm = self.gm
+        if cfg["kind"] == "nuts":
+            mean, cov = dense_gauss_32()
+            s = gm.NUTS(gm.DenseGaussian(mean, cov), x0, cfg["target_accept"], dtype=dt,
+                        max_depth=cfg["max_depth"], chain_offset=offset).set_seed(seed)
+            if cfg.get("mass"):
+                s.set_mass_adaptation(gm.NUTSMassMatrixConfig(cfg["mass"]))
+            return s
+        if cfg["kind"] == "hmc":
+            return gm.HMC(gm.RosenbrockND(), x0, cfg["eps"], cfg["L"], dtype=dt, chain_offset=offset).set_seed(seed)
+        return gm.MetropolisHastings(gm.IsotropicGaussian(1.0), gm.IsotropicGaussian(cfg["proposal_std"]),
+                                     x0, dtype=dt, chain_offset=offset).seed(seed)
 
     def sampler(self, x0, offset):
         a = self.a
@@ -486,8 +506,9 @@ def config_summary(name, cfg, figs, world, rhat, ess):
         n_samp = cfg["n_collect"] - 1
         fa = 2 * D * D + 8 * D
         tf = fa * (lf / world) / (kms * 1e-3) / 1e12
+        mass = f", {cfg['mass']} mass-matrix adaptation" if cfg.get("mass") else ""
         out.update(workload=f"NUTS DenseGaussian dim={D} f64, {chains} chains, target_accept "
-                            f"{cfg['target_accept']}, max_depth {cfg['max_depth']}, run({cfg['n_collect']}, "
+                            f"{cfg['target_accept']}, max_depth {cfg['max_depth']}{mass}, run({cfg['n_collect']}, "
                             f"{cfg['n_discard']}) as run(1, {cfg['n_discard']}) + run({cfg['n_collect']}, 0)",
                    metric="leapfrog steps/s (sampling phase)", value=lf / t, value_kernel=lf / (kms * 1e-3),
                    leapfrogs=lf, mean_tree_leapfrogs=lf / (chains * n_samp),

@@ -161,7 +161,8 @@ def test_bench_line_world1_and_world2(tmp_path):
     assert l2["ess"]["cfg2_schedule"]["sampling_s"] == 0.02
     # the config legs: every rank's share, the slowest rank's time, work summed
     for line, world in ((l1, 1), (l2, 2)):
-        assert set(line["configs"]) == {"cfg3", "cfg4", "cfg5"}
+        assert set(line["configs"]) == {"cfg3", "cfg3_dense", "cfg4", "cfg5"}
+        assert "dense mass-matrix adaptation" in line["configs"]["cfg3_dense"]["workload"]
         c3 = line["configs"]["cfg3"]
         assert c3["chains_total"] == 8192 * world and c3["leapfrogs"] == 1000 * 8192 * world
         assert c3["wall_s"] == 0.1 * world and c3["value"] == c3["leapfrogs"] / c3["wall_s"]
