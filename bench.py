@@ -229,7 +229,9 @@ class GpuBench:
 
     def copy_ceiling(self, nbytes=1 << 30, reps=5):
         """Empirical HBM ceiling on this box: a 1 GiB
-        device-to-device copy, read + write bytes over the median time."""
+        device-to-device copy by the engine's 16-byte copy kernel
+        (gm_memcpy_dtod, util_kernels.hip copy16_kernel), read + write bytes
+        over the median time."""
         import ctypes as C
         lib, _lib = self.lib, self._lib
         src, dst = C.c_void_p(), C.c_void_p()

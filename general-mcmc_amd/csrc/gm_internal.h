@@ -118,6 +118,8 @@ int build_target(const gm_target* t, gm_dtype dt, long long dim, TargetDev* out,
 
 // ---- utilities -------------------------------------------------------------
 // [rows][C][D] -> [C][rows][D]
+// dst = src in 16-byte words (both 16-byte aligned), util_kernels.hip
+hipError_t launch_copy16(const void* src, void* dst, long long words, hipStream_t st);
 hipError_t launch_transpose_samples(gm_dtype dt, const void* src, void* dst, long long rows,
                                     long long C, long long D, hipStream_t st);
 

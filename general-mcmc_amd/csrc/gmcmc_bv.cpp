@@ -60,6 +60,10 @@ int gm_memcpy_dtoh(void* dst, const void* src, size_t bytes) {
 int gm_memcpy_dtod(void* dst, const void* src, size_t bytes) {
   if (bytes == 0) return GM_OK;
   BV_REQ(dst && src, "NULL pointer");
+  // 16-byte aligned buffers of a whole number of 16-byte words (the
+  // allocator's buffers): the engine's own copy kernel; otherwise the runtime
+  if ((((uintptr_t)dst | (uintptr_t)src | (uintptr_t)bytes) & 15) == 0)
+    return bv_status(launch_copy16(src, dst, (long long)(bytes / 16), nullptr), "copy16");
   return bv_status(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, nullptr), "hipMemcpy D2D");
 }
 

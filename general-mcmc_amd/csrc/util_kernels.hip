@@ -91,6 +91,33 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ sr
   }
 }
 
+// Device-to-device copy in 16-byte words (assign, euclidean.rs:380-382):
+// each thread moves 4 words per pass, its loads issued together before the
+// stores, 1024 words per block pass and at most 8192 blocks (32 per CU), so
+// HBM sees full 64-byte lines from every wave.
+__global__ __launch_bounds__(256) void copy16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                     long long n) {
+  const long long stride = (long long)gridDim.x * 1024;
+  for (long long i = (long long)blockIdx.x * 1024 + threadIdx.x; i < n; i += stride) {
+    uint4 w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * 256 < n) w[u] = src[i + u * 256];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * 256 < n) dst[i + u * 256] = w[u];
+  }
+}
+
+hipError_t launch_copy16(const void* src, void* dst, long long words, hipStream_t st) {
+  if (words <= 0) return hipSuccess;
+  long long blocks = (words + 1023) / 1024;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(copy16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const uint4*)src, (uint4*)dst,
+                     words);
+  return hipGetLastError();
+}
+
 hipError_t launch_transpose_samples(gm_dtype dt, const void* src, void* dst, long long rows,
                                     long long C, long long D, hipStream_t st) {
   const long long total = rows * C * D;

@@ -188,3 +188,28 @@ def test_euclidean_scale_fill_dot(bv, dtype):
     bv.fill(dy, 2.5)
     assert (dy.to_host() == dtype(2.5)).all()
     assert bv.dot(bv.DeviceMatrix((0,), dtype), bv.DeviceMatrix((0,), dtype)) == 0.0
+
+
+@pytest.mark.parametrize("nbytes,off", [(16, 0), (4096 * 16 + 16, 0), ((1 << 24) + 48, 0), (1000, 0), (4096, 8),
+                                        (17, 3)])
+def test_memcpy_dtod_sizes_and_alignment(gm, nbytes, off):
+    """assign (euclidean.rs:380-382) through gm_memcpy_dtod: the 16-byte copy
+    kernel for aligned whole-word buffers (partial last pass included), the
+    runtime copy otherwise (odd sizes, 8-byte offsets); every byte equal."""
+    import ctypes as C
+    lib, _lib = gm._lib.load(), gm._lib
+    rng = np.random.default_rng(nbytes)
+    h = rng.integers(0, 256, nbytes + off, dtype=np.uint8)
+    src, dst = C.c_void_p(), C.c_void_p()
+    _lib.check(lib.gm_malloc(C.byref(src), nbytes + off))
+    _lib.check(lib.gm_malloc(C.byref(dst), nbytes + off))
+    try:
+        _lib.check(lib.gm_memcpy_htod(src, h.ctypes.data, nbytes + off))
+        _lib.check(lib.gm_memcpy_dtod(C.c_void_p(dst.value + off), C.c_void_p(src.value + off), nbytes))
+        _lib.check(lib.gm_device_synchronize())
+        out = np.zeros(nbytes + off, np.uint8)
+        _lib.check(lib.gm_memcpy_dtoh(out.ctypes.data, C.c_void_p(dst.value + off), nbytes))
+        np.testing.assert_array_equal(out[:nbytes], h[off:off + nbytes])
+    finally:
+        lib.gm_free(src)
+        lib.gm_free(dst)
