@@ -60,8 +60,15 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
       const T ex = (i < D) ? div_by_const(-(d * d), two_var, inv_two_var) : (T)0;
       qpart = (e == 0) ? ex : qpart + ex;
     }
-    const T logq = group_sum<LPC>(qpart) + qconst;
-    const T lp1 = tg.template eval<LPC, E, true>(y, gdummy, lane);
+    // the proposal density's sum and the target's, reduced together: the
+    // same stages (and bits) as two group_sums, each stage's DPP latency
+    // covered by the other sum instead of wait states
+    T sums[2];
+    sums[0] = qpart;
+    sums[1] = tg.template eval_part<LPC, E>(y, gdummy, lane);
+    group_sum_n<LPC>(sums);
+    const T logq = sums[0] + qconst;
+    const T lp1 = tg.finish(sums[1]);
     const T log_alpha = (lp1 + logq) - (lp + logq);
     T lnu;
     if constexpr (LPC == 64) {
