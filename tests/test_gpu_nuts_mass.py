@@ -83,17 +83,23 @@ def test_dense_warmup_wide_layout(gm, oracle):
                    initial_window=10)
 
 
-def test_dense_warmup_matrix_core_layout(gm, oracle):
-    """D = 20 f64 runs at 16 lanes x 2 (the dense Gaussian's product on the
-    matrix cores), with the dense metric's transposed per-chain matrices and
-    column batches (20 = 8 + 8 + 4); 10 chains leave the last wave half
-    empty (the VALU product there)."""
+@pytest.mark.parametrize("minv_lds,chol_lds", [("2", "1"), ("1", "1"), ("1", "0"), ("0", "0")])
+@pytest.mark.parametrize("D,chains", [(20, 10), (32, 36)])
+def test_dense_warmup_matrix_core_layout(gm, oracle, monkeypatch, minv_lds, chol_lds, D, chains):
+    """f64 at 16 lanes x 2 (the dense Gaussian's product on the matrix cores)
+    with each form of the dense metric's products: M^-1 full in LDS (2), its
+    packed lower triangle with or without the packed Cholesky factor (1), and
+    the transposed per-chain matrices in global memory (0)
+    (GMCMC_NUTS_MINV_LDS / GMCMC_NUTS_CHOL_LDS, nuts_launch.h); D = 20 pads
+    rows and columns to 32, and 10 or 36 chains leave the last wave partly
+    empty (the VALU target product there)."""
+    monkeypatch.setenv("GMCMC_NUTS_MINV_LDS", minv_lds)
+    monkeypatch.setenv("GMCMC_NUTS_CHOL_LDS", chol_lds)
     rng = np.random.default_rng(21)
-    D = 20
     a = rng.standard_normal((D, D))
     cov = a @ a.T / D + 0.5 * np.eye(D)
     t = _gauss(gm, cov, rng.standard_normal(D))
-    x0 = gm.init_with_seed(10, D, 6, np.float64)
+    x0 = gm.init_with_seed(chains, D, 6, np.float64)
     s, om = _check_run(gm, oracle, t, x0, np.float64, 2, [(8, 45), (6, 20)], start_buffer=4, end_buffer=4,
                        initial_window=10)
     assert s.layout() == (16, 2)
