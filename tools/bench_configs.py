@@ -45,6 +45,8 @@ def cfg3(a):
         s.set_mass_adaptation(gm.NUTSMassMatrixConfig(a.nuts_mass))
     if a.nuts_layout:
         s.set_layout(*[int(v) for v in a.nuts_layout.split("x")])
+    if a.nuts_lds_levels >= 0:
+        s.set_lds_levels(a.nuts_lds_levels)
     # warm-up (step-size adaptation) then sampling, as NUTS::run_progress
     _, tw = timed(lambda: s.run_positions(1, a.nuts_discard))
     lf0 = s.leapfrog_counts().sum()
@@ -108,6 +110,7 @@ def main():
     p.add_argument("--nuts-mass", default="none", choices=["none", "diagonal", "dense"],
                    help="cfg3 with the warm-up metric adaptation (new_with_mass_matrix)")
     p.add_argument("--nuts-chains", type=int, default=8192)
+    p.add_argument("--nuts-lds-levels", type=int, default=-1, help="cap on the subtree-stack levels held in LDS")
     p.add_argument("--nuts-discard", type=int, default=500)
     p.add_argument("--nuts-collect", type=int, default=500)
     p.add_argument("--nuts-layout", default="")
