@@ -148,10 +148,12 @@ class GpuBench:
             # not include the kernel's first-launch cost (code-object load; 3-4
             # ms on the cfg5 MH leg before this warm-up, profiles/r03/final)
             w = self._same_kind(cfg, dt, x0, offset, 7)
-            w.set_layout(*s.layout())
-            w.run_positions(1, 0)
-            self.sync()
-            w.close()
+            try:
+                w.set_layout(*s.layout())
+                w.run_positions(1, 0)
+                self.sync()
+            finally:
+                w.close()
             s.reserve(cfg["n_collect"])
             lf0 = int(s.leapfrog_counts().sum())
             self.sync()
