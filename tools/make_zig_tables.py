@@ -1,14 +1,15 @@
 """Ziggurat tables for the standard normal (Marsaglia & Tsang 2000, 256 layers)
-used by the engine's f64 MH proposal normals (RNG spec).
+of the round-3 experiment that drew the f64 MH proposal normals by the
+ziggurat (measured slower than Box-Muller on the GPU and not kept:
+profiles/r03/ab/summary.json).
 
 f(x) = exp(-x^2/2) on x >= 0 is covered by 256 layers of equal area v: layer
 0 is the base strip [0, r) x [0, f(r)) plus the tail beyond r (its "width"
 X[0] = v / f(r)), layer i >= 1 spans [0, X[i]) x [F[i], F[i+1]) with
 X[1] = r, X[i+1] = sqrt(-2 ln(v / X[i] + F[i])), X[256] = 0, F[i] = f(X[i]),
 F[256] = 1. r is solved (bisection, f64) so that the top layer's area
-X[255] (1 - F[255]) equals v. The tables are data: the kernel (gm_rng.h)
-and the oracle (oracle/gm_oracle.c) hold the same hex literals, written by
-this script; tests/test_oracle_rng.py checks that they agree.
+X[255] (1 - F[255]) equals v. The experiment compiled the hex literals this
+script prints into both the kernel and the oracle.
 
     python tools/make_zig_tables.py   # prints the C initializers
 """
