@@ -499,6 +499,62 @@ template <class T> GM_HD T exp1(uint64_t seed, uint32_t chain, uint64_t step, ui
   return -glog_pos(uniform_oc<T>(seed, chain, step, tag, idx));
 }
 
+// ---- table-driven f64 Box-Muller (spec v5: the f64 MH proposal normals) ---
+// The same pairs as normals_of (z0 = r cos 2 pi u2, z1 = r sin 2 pi u2,
+// r = sqrt(-2 ln u1), u1 in (0,1], u2 in [0,1) from the block's two word
+// pairs), with ln and sin/cos from tables (gm_bm_tables.h,
+// tools/make_bm_tables.py) instead of msun's polynomials and division:
+//   ln u1 = e ln2 + ln c_j + ln(1 + r),  r = fma(m, 1/c_j, -1), |r| < 2^-8,
+//     m in [1,2) the significand, j its top 7 bits, ln(1 + r) to degree 6;
+//   2 pi u2 = 2 pi j/256 + th, th in [0, 2 pi/256): sin/cos(2 pi j/256) from
+//     the table, sin th to degree 7, cos th - 1 to degree 6, angle addition.
+#include "gm_bm_tables.h"
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+static __constant__ double gm_bm_log[256] = {GM_BM_LOG_INIT};
+static __constant__ double gm_bm_sincos[512] = {GM_BM_SINCOS_INIT};
+typedef double gm_bm_d2 __attribute__((ext_vector_type(2)));
+struct BmLds {  // the tables as 16-byte pairs in LDS
+  gm_bm_d2 lg[128], sc[256];
+};
+__device__ __forceinline__ void bm_lds_fill(BmLds& t) {
+  for (int k = threadIdx.x; k < 256; k += blockDim.x) {
+    if (k < 128) t.lg[k] = gm_bm_d2{gm_bm_log[2 * k], gm_bm_log[2 * k + 1]};
+    t.sc[k] = gm_bm_d2{gm_bm_sincos[2 * k], gm_bm_sincos[2 * k + 1]};
+  }
+}
+__device__ __forceinline__ void normals_tab(u32x4 x, double (&z)[2], const BmLds& t) {
+  // ln u1
+  const double u1 = Unif<double>::oc(x.x, x.y);
+  const uint64_t b = d2u(u1);
+  const int e = (int)(b >> 52) - 1023;
+  const uint64_t mb = b & 0x000fffffffffffffull;
+  const double m = u2d(mb | 0x3ff0000000000000ull);
+  const gm_bm_d2 lc = t.lg[(int)(mb >> 45)];
+  const double r = __builtin_fma(m, lc.x, -1.0);
+  double p = __builtin_fma(r, -0x1.5555555555555p-3, 0x1.999999999999ap-3);
+  p = __builtin_fma(r, p, -0.25);
+  p = __builtin_fma(r, p, 0x1.5555555555555p-2);
+  p = __builtin_fma(r, p, -0.5);
+  const double l1 = __builtin_fma(r * r, p, r);
+  const double de = (double)e;
+  const double lnu = __builtin_fma(de, 0x1.62e42fefa39efp-1, __builtin_fma(de, 0x1.abc9e3b39803fp-56, lc.y + l1));
+  const double rad = gsqrt(-2.0 * lnu);
+  // sin / cos of 2 pi u2
+  const double u2 = Unif<double>::co(x.z, x.w);
+  const int j = (int)(u2 * 256.0);
+  const double th = (u2 - (double)j * 0.00390625) * 0x1.921fb54442d18p+2;
+  const double zz = th * th;
+  const double sth = __builtin_fma(th * zz, __builtin_fma(zz, __builtin_fma(zz, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7),
+                                                          -0x1.5555555555555p-3), th);
+  const double cm = zz * __builtin_fma(zz, __builtin_fma(zz, -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5), -0.5);
+  const gm_bm_d2 sc = t.sc[j];
+  const double sv = __builtin_fma(sc.y, sth, __builtin_fma(sc.x, cm, sc.x));
+  const double cv = __builtin_fma(-sc.x, sth, __builtin_fma(sc.y, cm, sc.y));
+  z[0] = rad * cv;
+  z[1] = rad * sv;
+}
+#endif
+
 // A per-lane cache of one block of draws for consecutive steps.
 template <class T> struct NormalCache {
   T z[Blk<T>::S];

@@ -14,6 +14,14 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   const long long c = gtid / LPC;
   const int lane = (int)(gtid % LPC);
   const auto tg = tg_.template bind<LPC, E>(lane);  // per-lane target view
+  // f64 proposals: the table-driven Box-Muller (gm_rng.h normals_tab); its
+  // tables in LDS, filled by the whole block before any thread returns
+  constexpr bool TAB = sizeof(T) == 8;
+  __shared__ BmLds bm_lds[1];
+  if constexpr (TAB) {
+    bm_lds_fill(bm_lds[0]);
+    __syncthreads();
+  }
   if (c >= a.C) return;
   const int D = a.D;
   T* __restrict__ qs = (T*)a.q;
@@ -36,7 +44,16 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   }
   T lp = tg.template eval<LPC, E, true>(x, gdummy, lane);
   long long acc = 0;
-  NormalCache<T> ncache[E];
+  NormalCache<T> ncache[E];  // f32: msun Box-Muller
+  // f64: the table-driven Box-Muller pair of each coordinate's current block
+  // (two steps), as plain per-coordinate values (selected, never indexed)
+  double tz0[E], tz1[E];
+  uint64_t tblk[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    tz0[e] = tz1[e] = 0.0;
+    tblk[e] = ~0ull;
+  }
   UniformCache<T> ucache;
   uint64_t lblk = ~0ull;  // LPC == 64: the draw block whose accept logs lnl holds (lane k: step k)
   T lnl = (T)0;
@@ -50,7 +67,18 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
       if (i < D) {
-        const T n = ncache[e].get(a.seed, cid, st, TAG_MH_PROP, (uint32_t)i);
+        T n;
+        if constexpr (TAB) {
+          if (st / 2 != tblk[e]) {
+            double z[2];
+            normals_tab(draw_block(a.seed, cid, st / 2, TAG_MH_PROP, (uint32_t)i), z, bm_lds[0]);
+            tz0[e] = z[0];
+            tz1[e] = z[1];
+            tblk[e] = st / 2;
+          }
+          n = (st & 1u) ? tz1[e] : tz0[e];
+        }
+        else n = ncache[e].get(a.seed, cid, st, TAG_MH_PROP, (uint32_t)i);
         y[e] = x[e] + n * sd;
       } else {
         y[e] = (T)0;

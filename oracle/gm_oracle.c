@@ -230,6 +230,47 @@ double or_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, u
   sincos2pi_d(unif_co_d(x[2], x[3]), &c, &s);
   return (step % 2 == 0) ? r * c : r * s;
 }
+/* Spec v5, the f64 MH proposal normals: the same Box-Muller pairs with ln and
+ * sin/cos from tables (gm_bm_tables.h, tools/make_bm_tables.py):
+ * ln u1 = e ln2 + ln c_j + ln(1 + r), r = fma(m, 1/c_j, -1); 2 pi u2 =
+ * 2 pi j/256 + th, angle addition with degree-7 sin th and degree-6 cos th - 1. */
+#include "gm_bm_tables.h"
+static const double bm_log[256] = {GM_BM_LOG_INIT};
+static const double bm_sincos[512] = {GM_BM_SINCOS_INIT};
+double or_tab_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  uint32_t x[4];
+  block(seed, chain, step / 2, tag, idx, x);
+  const double u1 = unif_oc_d(x[0], x[1]);
+  const uint64_t b = bits_d(u1);
+  const int e = (int)(b >> 52) - 1023;
+  const uint64_t mb = b & 0x000fffffffffffffull;
+  const double m = from_bits_d(mb | 0x3ff0000000000000ull);
+  const int jl = (int)(mb >> 45);
+  const double invc = bm_log[2 * jl], logc = bm_log[2 * jl + 1];
+  const double r = fma(m, invc, -1.0);
+  double p = fma(r, -0x1.5555555555555p-3, 0x1.999999999999ap-3);
+  p = fma(r, p, -0.25);
+  p = fma(r, p, 0x1.5555555555555p-2);
+  p = fma(r, p, -0.5);
+  const double l1 = fma(r * r, p, r);
+  const double de = (double)e;
+  const double lnu = fma(de, 0x1.62e42fefa39efp-1, fma(de, 0x1.abc9e3b39803fp-56, logc + l1));
+  const double rad = sqrt(-2.0 * lnu);
+  const double u2 = unif_co_d(x[2], x[3]);
+  const int j = (int)(u2 * 256.0);
+  const double th = (u2 - (double)j * 0.00390625) * 0x1.921fb54442d18p+2;
+  const double zz = th * th;
+  const double sth = fma(th * zz, fma(zz, fma(zz, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7), -0x1.5555555555555p-3), th);
+  const double cm = zz * fma(zz, fma(zz, -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5), -0.5);
+  const double S = bm_sincos[2 * j], Cc = bm_sincos[2 * j + 1];
+  const double sv = fma(Cc, sth, fma(S, cm, S));
+  const double cv = fma(-S, sth, fma(Cc, cm, Cc));
+  return (step % 2 == 0) ? rad * cv : rad * sv;
+}
+float or_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
+static float or_mh_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  return or_normal_f(seed, chain, step, tag, idx);
+}
 float or_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
   uint32_t x[4];
   block(seed, chain, step / 4, tag, idx, x);
@@ -335,6 +376,7 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #define SQRT sqrt
 #define FMA fma
 #define NORMAL or_normal_d
+#define MH_NORMAL or_tab_normal_d
 #define UNIF_CO or_uniform_co_d
 #define UNIF_OC uniform_oc_d
 #define NUTS_U or_nuts_u_d
@@ -348,6 +390,7 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #undef SQRT
 #undef FMA
 #undef NORMAL
+#undef MH_NORMAL
 #undef UNIF_CO
 #undef UNIF_OC
 #undef NUTS_U
@@ -361,6 +404,7 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #define SQRT sqrtf
 #define FMA fmaf
 #define NORMAL or_normal_f
+#define MH_NORMAL or_mh_normal_f
 #define UNIF_CO or_uniform_co_f
 #define UNIF_OC uniform_oc_f
 #define NUTS_U or_nuts_u_f

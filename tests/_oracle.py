@@ -48,6 +48,9 @@ def load():
         getattr(lib, f"or_cos2pi_{sfx}").argtypes = [rt]
         getattr(lib, f"or_normal_{sfx}").restype = rt
         getattr(lib, f"or_normal_{sfx}").argtypes = [_u64, _u32, _u64, _u32, _u32]
+        if sfx == "d":
+            lib.or_tab_normal_d.restype = rt
+            lib.or_tab_normal_d.argtypes = [_u64, _u32, _u64, _u32, _u32]
         getattr(lib, f"or_uniform_co_{sfx}").restype = rt
         getattr(lib, f"or_uniform_co_{sfx}").argtypes = [_u64, _u32, _u64, _u32, _u32]
         getattr(lib, f"or_logp_grad_{sfx}").restype = rt

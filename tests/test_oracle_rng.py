@@ -60,6 +60,33 @@ def test_normal_stream_moments(oracle, sfx):
     assert abs(np.mean(z ** 4) - 3) < 0.15
 
 
+def test_tab_normal_pairs_and_moments(oracle):
+    """Spec v5 (the f64 MH proposal normals): table-driven Box-Muller pairs.
+    Steps 2k and 2k+1 share one Philox block (z0, z1 of one pair); the values
+    agree with the msun-polynomial Box-Muller of the same block to a few ulps
+    of the radius; the engine and the oracle read one generated table file."""
+    import os
+    lib = oracle.lib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "oracle", "gm_bm_tables.h")) as f:
+        a = f.read()
+    with open(os.path.join(root, "general-mcmc_amd", "csrc", "gm_bm_tables.h")) as f:
+        assert f.read() == a
+    z = np.array([[lib.or_tab_normal_d(7, c, s, 4, d) for s in range(8)]
+                  for c in range(60) for d in range(50)])
+    msun = np.array([[lib.or_normal_d(7, c, s, 4, d) for s in range(8)]
+                     for c in range(60) for d in range(50)])
+    assert np.max(np.abs(z - msun)) < 1e-13
+    assert not np.array_equal(z[:, 0], z[:, 1])  # the pair's two members
+    zz = z.ravel()
+    assert abs(zz.mean()) < 0.02
+    assert abs(zz.std() - 1) < 0.02
+    assert abs(np.mean(zz ** 3)) < 0.1  # sd of the sample skewness: sqrt(15 / 24000) = 0.025
+    assert abs(np.mean(zz ** 4) - 3) < 0.3
+    # u1 near 1 (rad -> 0) and tiny u1 (the tail) stay finite
+    assert np.all(np.isfinite(z))
+
+
 def test_nuts_stream_mix64_splitmix_kat(oracle):
     """The NUTS per-transition draws hash K + (idx + 1) * 0x9E3779B97F4A7C15
     with the SplitMix64 finalizer: K = 1234567 reproduces the published

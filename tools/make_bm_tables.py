@@ -1,0 +1,40 @@
+"""Tables of the table-driven f64 Box-Muller (RNG spec v5, the f64 MH proposal
+normals): 128 (1/c_j, ln c_j) pairs, c_j = 1 + (j + 1/2)/128, for
+ln m = ln c_j + ln(1 + (m/c_j - 1)) on m in [1, 2); 256 (sin, cos)(2 pi j/256)
+pairs for the angle-addition sin/cos. Written as C initializers (hex
+literals): the kernel (gm_bm_tables.h) and the oracle hold the same data.
+
+    python tools/make_bm_tables.py > general-mcmc_amd/csrc/gm_bm_tables.h
+"""
+import math
+
+
+def main():
+    print("// gm_bm_tables.h -- tables of the f64 table-driven Box-Muller (RNG spec v5),")
+    print("// written by tools/make_bm_tables.py; oracle/gm_bm_tables.h is the same file.")
+    print("#pragma once")
+    lg = []
+    for j in range(128):
+        c = 1.0 + (j + 0.5) / 128.0
+        lg += [1.0 / c, math.log(c)]
+    print("#define GM_BM_LOG_INIT \\")
+    for k in range(0, len(lg), 4):
+        print("  " + ", ".join(v.hex() for v in lg[k:k + 4]) + (", \\" if k + 4 < len(lg) else " \\"))
+    print("")
+    sc = []
+    for j in range(256):
+        a = 2.0 * math.pi * j / 256.0
+        sc += [math.sin(a), math.cos(a)]
+    # exact values where they are exact
+    for j in range(256):
+        if j % 64 == 0:
+            q = j // 64
+            sc[2 * j], sc[2 * j + 1] = [(0.0, 1.0), (1.0, 0.0), (0.0, -1.0), (-1.0, 0.0)][q]
+    print("#define GM_BM_SINCOS_INIT \\")
+    for k in range(0, len(sc), 4):
+        print("  " + ", ".join(float(v).hex() for v in sc[k:k + 4]) + (", \\" if k + 4 < len(sc) else " \\"))
+    print("")
+
+
+if __name__ == "__main__":
+    main()
