@@ -150,6 +150,82 @@ __device__ __forceinline__ void full_cols(unsigned base, const T (&p)[E], T (&ac
   }
 }
 
+// Columns [J, J + NB) of p = L z from the global factor (cholT[j][i] = L_ij,
+// row stride D <= 32) when it is not resident in LDS (the full-M^-1 budget):
+// the batch's loads, clamped to valid addresses, and row broadcasts first,
+// then the sums in ascending j. Terms with j > i (L_ij = 0 there), padded
+// rows (i >= D) and padded columns (z_j = +0) add +-0 to the +0-started sum:
+// no bit changes, as in packed_cols.
+#ifndef GM_CHOL_BATCH
+#define GM_CHOL_BATCH 8
+#endif
+template <int LPC, int E, class T, int J>
+__device__ __forceinline__ void chol_global_cols(const T* const (&pb)[E], int D, const int (&r)[E],
+                                                 const T (&z)[E], T (&acc)[E]) {
+  constexpr int DP = LPC * E;
+  constexpr int NB = GM_CHOL_BATCH < DP - J ? GM_CHOL_BATCH : DP - J;
+  if constexpr (NB > 0) {
+    T m[NB][E], zj[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int j = (J + u < D) ? J + u : D - 1;
+#pragma unroll
+      for (int e = 0; e < E; ++e) m[u][e] = pb[e][j * D];
+    }
+    row_bcasts<E, T, J, 0, NB>(z, zj);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const T mm = (J + u > r[e] || r[e] >= D) ? (T)0 : m[u][e];
+        acc[e] = acc[e] + mm * zj[u];
+      }
+    }
+    chol_global_cols<LPC, E, T, J + NB>(pb, D, r, z, acc);
+  }
+}
+
+// full_cols software-pipelined (GM_FULL_PIPE = batch width): batch J + NB's
+// reads and broadcasts are issued before batch J's sums, so the LDS latency
+// of all but the first batch hides behind the dependent adds. Same sums.
+template <int LPC, int E, class T, int J, int NB>
+__device__ __forceinline__ void full_cols_load(unsigned base, const T (&p)[E],
+                                               T (&m)[NB][E], T (&pj)[NB]) {
+  constexpr int DP = LPC * E;
+  typedef T vE __attribute__((ext_vector_type(E)));
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const vE w = *(const vE*)(gm_dyn_lds + base + (J + u) * DP * sizeof(T));
+#pragma unroll
+    for (int e = 0; e < E; ++e) m[u][e] = w[e];
+  }
+  row_bcasts<E, T, J, 0, NB>(p, pj);
+}
+template <int LPC, int E, class T, int J, int NB>
+__device__ __forceinline__ void full_cols_pipe(unsigned base, const T (&p)[E], const T (&m)[NB][E],
+                                               const T (&pj)[NB], T (&acc)[E]) {
+  constexpr int DP = LPC * E;
+  if constexpr (J + NB < DP) {
+    T m2[NB][E], pj2[NB];
+    full_cols_load<LPC, E, T, J + NB, NB>(base, p, m2, pj2);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] = acc[e] + m[u][e] * pj[u];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    full_cols_pipe<LPC, E, T, J + NB, NB>(base, p, m2, pj2, acc);
+  } else {
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] = acc[e] + m[u][e] * pj[u];
+    }
+  }
+}
+
 // columns per batch of the dense products (their loads / broadcasts issued
 // together; the sums stay in ascending j). 4 keeps the dense-metric kernel
 // within 256 registers (2 waves per SIMD; 8 took it to 276 and 1 wave).
@@ -169,7 +245,15 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E, K>& M, const T (&p)[
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
     if constexpr (LPC == 16 && E == 2) {
       if (M.minv_lds == 2) {
+#ifdef GM_FULL_PIPE
+        static_assert((LPC * E) % GM_FULL_PIPE == 0, "batch width divides the padded dimension");
+        T m0[GM_FULL_PIPE][E], pj0[GM_FULL_PIPE];
+        const unsigned base = M.lds_off + (unsigned)(lane * E * (int)sizeof(T));
+        full_cols_load<LPC, E, T, 0, GM_FULL_PIPE>(base, p, m0, pj0);
+        full_cols_pipe<LPC, E, T, 0, GM_FULL_PIPE>(base, p, m0, pj0, acc);
+#else
         full_cols<LPC, E, T, 0>(M.lds_off + (unsigned)(lane * E * (int)sizeof(T)), p, acc);
+#endif
 #pragma unroll
         for (int e = 0; e < E; ++e) v[e] = acc[e];
         return;
@@ -246,6 +330,23 @@ __device__ __forceinline__ void momentum_from(const MassDev<T, E, K>& M, const T
         for (int e = 0; e < E; ++e) p[e] = acc[e];
         return;
       }
+#ifndef GM_CHOL_LOOP
+      {
+        int r[E];
+        const T* pb[E];  // row r's entries (clamped to a valid row); opaque, so
+                         // the column addresses are not hoisted out of the loop
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          r[e] = lane * E + e;
+          pb[e] = M.cholT + (r[e] < M.D ? r[e] : M.D - 1);
+          __asm__ volatile("" : "+v"(pb[e]));
+        }
+        chol_global_cols<LPC, E, T, 0>(pb, M.D, r, z, acc);
+#pragma unroll
+        for (int e = 0; e < E; ++e) p[e] = acc[e];
+        return;
+      }
+#endif
     }
     constexpr int GB = GM_DENSE_BATCH;
     for (int j0 = 0; j0 < M.D; j0 += GB) {  // batches of GB columns, as inv_mul
