@@ -123,6 +123,12 @@ class GpuBench:
         from general_mcmc_amd import _lib
         self.gm, self._lib, self.a, self.cp = gm, _lib, a, cp
         lib = _lib.load()
+        import ctypes
+        n_dev = ctypes.c_int(0)
+        _lib.check(lib.gm_device_count(ctypes.byref(n_dev)))
+        if cp.local_rank >= n_dev.value:
+            raise SystemExit(f"bench.py: rank {cp.rank} needs GPU {cp.local_rank} but {n_dev.value} "
+                             f"device(s) are visible (--gpus {a.gpus})")
         _lib.check(lib.gm_set_device(cp.local_rank))
         self.lib = _lib.require_gpu()
         self.dtype = np.float32 if a.dtype == "f32" else np.float64
@@ -562,6 +568,9 @@ def main(argv=None, backend=None):
 
     cp = ControlPlane()  # gloo control plane when launched by torchrun
     world, rank = cp.world, cp.rank
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started {world} rank(s) "
+                         f"(WORLD_SIZE={os.environ.get('WORLD_SIZE')})")
     be = (backend or GpuBench)(a, cp)
     s_bytes = 4 if a.dtype == "f32" else 8
     D, L = a.dim, a.leapfrog
@@ -571,6 +580,8 @@ def main(argv=None, backend=None):
     sampler = be.sampler(x0, offset)
     lanes, elems = sampler.layout()
     comm = be.comm()
+    if world > 1 and (comm is None or comm.info()["nranks"] != world):
+        raise SystemExit(f"bench.py: the RCCL communicator does not span the {world} ranks")
 
     def barrier_sync():
         be.sync()
@@ -730,5 +741,42 @@ def main(argv=None, backend=None):
     return line
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(argv, n: int) -> int:
+    """`bench.py --gpus N` (N > 1) started as one plain process: start the N
+    ranks as `torch.distributed.run` children (one process per GPU, rendezvous
+    on 127.0.0.1) and return their exit status. Nothing here touches the GPU
+    or imports the engine, so the children are the only HIP processes; rank 0
+    prints the line to the inherited stdout."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    return subprocess.run(cmd).returncode
+
+
+def backend_from_env():
+    """GMCMC_BENCH_BACKEND=module:factory replaces GpuBench (CPU tests of the
+    CLI path, tests/test_bench_cpu.py); unset in every real run."""
+    spec = os.environ.get("GMCMC_BENCH_BACKEND")
+    if not spec:
+        return None
+    import importlib
+    mod, fn = spec.split(":")
+    return getattr(importlib.import_module(mod), fn)()
+
+
 if __name__ == "__main__":
-    main()
+    _args = parse()
+    if _args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if _args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(sys.argv[1:], _args.gpus))
+    main(backend=backend_from_env())

@@ -126,6 +126,39 @@ def _worker(rank, world, port, outdir):
         assert line is None
 
 
+def _cli(args, extra_env=None, timeout=300):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(GMCMC_BENCH_BACKEND="tests.test_bench_cpu:stub_backend", **(extra_env or {}))
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_cli_gpus2_launches_two_ranks():
+    """The driver's own command form, `python bench.py --gpus 2`, started as
+    one plain process: bench.py must start two ranks itself (torch.distributed
+    .run children) and rank 0's line must describe a 2-rank job."""
+    r = _cli(ARGV + ["--gpus", "2"])
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2
+    assert [p["rank"] for p in line["timing"]["per_rank"]] == [0, 1]
+    assert line["rccl"]["nranks"] == 2
+    assert line["configs"]["cfg3"]["chains_total"] == 2 * 8192
+    assert line["config"]["parallelism"] == "chains sharded x2"
+
+
+def test_bench_cli_rank_count_mismatch_fails():
+    """A launcher that started fewer ranks than --gpus asks for is an error,
+    never a silent N = 1 line."""
+    r = _cli(ARGV + ["--gpus", "2"], extra_env={"WORLD_SIZE": "1"})
+    assert r.returncode != 0
+    assert "--gpus 2" in r.stderr and not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
 def _keys(d, prefix=""):
     out = set()
     for k, v in d.items():
