@@ -58,6 +58,8 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="target CPU time of each CPU-baseline sample (0 disables)")
     p.add_argument("--cpu-threads", type=int, default=0, help="0: every core available to this process")
+    p.add_argument("--cpu-config-seconds", type=float, default=3.0,
+                   help="target CPU time of each config leg's CPU-baseline sample (0 disables)")
     p.add_argument("--device-warmup-ms", type=float, default=50.0,
                    help="untimed scratch launches of the timed shape for this long before the W warm-up "
                         "transitions: the GPU clock ramps to its peak within ~10-30 ms of load "
@@ -442,6 +444,109 @@ def cpu_baseline(a, dtype, x0, lanes, elems):
     return out
 
 
+def _timed_scaled(run_once, seconds):
+    """Time run_once(k) (k units of work, returns the work done) at a k
+    calibrated so that the timed call takes about `seconds`."""
+    k, work = 1, None
+    while True:
+        t0 = time.perf_counter()
+        work = run_once(k)
+        dt = time.perf_counter() - t0
+        if dt >= 0.2 * seconds or k >= 1 << 20:
+            break
+        k = max(k + 1, int(k * min(64.0, 0.5 * seconds / max(dt, 1e-4))))
+    if dt < 0.5 * seconds:
+        k = max(k + 1, int(k * seconds / max(dt, 1e-4)))
+        t0 = time.perf_counter()
+        work = run_once(k)
+        dt = time.perf_counter() - t0
+    return k, work, dt
+
+
+def config_cpu_baseline(name, cfg, threads, seconds):
+    """The reference's CPU path for one BASELINE config leg, timed on this
+    host at `threads` threads and at 1 thread on a bounded sample (about
+    `seconds` each): the C restatements in oracle/ (gm_oracle.c, bit-matching,
+    threads over chain blocks as rayon's par_iter over chains, core.rs:221-225
+    and generic_nuts.rs:404-412), in the leg's own unit.
+      NUTS (cfg3): NUTS::step after step-size warm-up, generic_nuts.rs:755-925;
+      NUTS dense (cfg3_dense): GenericNUTS::new_with_mass_matrix's whole run,
+        dense warm-up included (the leg's whole_run rate);
+      HMC (cfg4): oracle/cpu_hmc.c (batched_hmc.rs:129-190 op structure, -O3);
+      MH (cfg5): metropolis_hastings.rs:306-318."""
+    from tests import _oracle
+    ora = _oracle.load()
+    D = cfg["dim"]
+    dt = np.float32 if cfg["dtype"] == "f32" else np.float64
+    out = {"kind": "port", "cores": threads}
+
+    def both(run, unit, what):
+        res = {}
+        for th in (threads, 1):
+            k, work, secs = _timed_scaled(lambda k: run(k, th), seconds)
+            res[th] = (work / secs, k, secs)
+        v, k, secs = res[threads]
+        out.update(value=v, unit=unit, sample=what(k, threads, secs))
+        v1, k1, s1 = res[1]
+        out["one_thread"] = {"value": v1, "cores": 1, "sample": what(k1, 1, s1)}
+        return out
+
+    if cfg["kind"] == "nuts":
+        mean, cov = dense_gauss_32()
+        prec = np.linalg.inv(cov)
+        t = _oracle.Target(3, D, mean=mean, prec=prec, norm_const=0.0)
+        lanes, elems = 16, 2
+        if cfg.get("mass"):
+            nd = 500  # the leg's warm-up: the default windows end at 450 (generic_nuts.rs:81-359)
+
+            def run(k, th):
+                C_ = k * th
+                x0 = np.random.default_rng(1).standard_normal((C_, D)).astype(dt)
+                st = ora.nuts_state(C_, dt)
+                mass = ora.nuts_mass(2, C_, D, dt)
+                _, _, _, nlf = ora.nuts_mass_run(t, x0, st, mass, cfg["target_accept"], cfg["max_depth"], 42, 0,
+                                                 20, nd, False, lanes, elems, threads=th)
+                return float(nlf.sum())
+            return both(run, "leapfrog steps/s (whole run, dense warm-up included)",
+                        lambda k, th, s: f"{k * th} chains x run(20, {nd}) with dense mass-matrix adaptation, "
+                                         f"oracle/gm_oracle.c or_nuts_mass_run, {th} thread(s), {s:.1f}s")
+        C_ = 4 * threads
+        x0 = np.random.default_rng(1).standard_normal((C_, D)).astype(dt)
+        st = ora.nuts_state(C_, dt)
+        q, _, _, _ = ora.nuts_run(t, x0, st, cfg["target_accept"], cfg["max_depth"], 42, 0, 1, 100, False,
+                                  lanes, elems, threads=threads)  # step-size warm-up (untimed)
+
+        def run(k, th):
+            s2 = {kk: np.array(v, copy=True) for kk, v in st.items()}
+            _, _, nlf = ora.nuts_step(t, q, s2, cfg["target_accept"], cfg["max_depth"], 42, 1000, k, 100, 100,
+                                      lanes, elems, threads=th)
+            return float(nlf.sum())
+        return both(run, "leapfrog steps/s (sampling phase)",
+                    lambda k, th, s: f"{C_} chains x {k} sampling transitions after 100 warm-up, "
+                                     f"oracle/gm_oracle.c or_nuts_step, {th} thread(s), {s:.1f}s")
+    if cfg["kind"] == "hmc":
+        fast = _oracle.cpu_hmc()
+        C_ = cfg["chains"]
+        q = np.random.default_rng(1).standard_normal((C_, D)).astype(np.float32)
+
+        def run(k, th):
+            fast.run(q, cfg["eps"], cfg["L"], k, 42, th)
+            return float(C_ * cfg["L"] * k)
+        return both(run, "chain-leapfrog steps/s",
+                    lambda k, th, s: f"{C_} chains x {k} transitions x {cfg['L']} leapfrogs, oracle/cpu_hmc.c "
+                                     f"(-O3, reference op structure), {th} thread(s), {s:.1f}s")
+    C_ = cfg["chains"]
+    x0 = np.random.default_rng(1).standard_normal((C_, D)).astype(dt)
+    t = _oracle.Target(2, D, std=1.0)
+
+    def run(k, th):
+        ora.mh_run(t, x0, cfg["proposal_std"], 42, 0, k, k, 64, 4, threads=th)
+        return float(C_ * k)
+    return both(run, "chain-steps/s",
+                lambda k, th, s: f"{C_} chains x {k} steps, oracle/gm_oracle.c or_mh_run (f64, bit-matching), "
+                                 f"{th} thread(s), {s:.1f}s")
+
+
 def load_pmc(C, D, L, dtype, steps):
     """PMC figures of the timed hmc_kernel launch from profiles/r02
     (tools/pmc_hmc.py over rocprofv3 passes of the driver's command). A
@@ -665,6 +770,11 @@ def main(argv=None, backend=None):
         extra["host_output"] = be.host_output(sampler)
         extra["north_star_check"] = be.north_star_check(offset=offset) if a.north_star else None
         extra["cpu_baseline"] = be.cpu_baseline(x0, lanes, elems) if a.cpu_seconds > 0 else None
+        if a.cpu_config_seconds > 0:
+            threads = a.cpu_threads or available_cores()[0]
+            for name in configs:
+                configs[name]["cpu_baseline"] = config_cpu_baseline(name, CONFIG_LEGS[name], threads,
+                                                                    a.cpu_config_seconds)
     cp.barrier()
 
     line = None

@@ -88,6 +88,8 @@ SIGNATURES = {
     "gm_nuts_get_step_size": (_ip, [_vp, _vp, _vp]),
     "gm_nuts_set_mass_adaptation": (_ip, [_vp, _i32, _i64, _i64, _i64, _dbl, _dbl, _i64]),
     "gm_nuts_set_lds_levels": (_ip, [_vp, _i32]),
+    "gm_nuts_set_dense_forms": (_ip, [_vp, _i32, _i32]),
+    "gm_nuts_get_plan": (_ip, [_vp, _vp]),
     "gm_nuts_get_mass": (_ip, [_vp, C.POINTER(_i32), _vp, _vp, _vp, _vp, _vp]),
     "gm_sampler_layout": (_ip, [_vp, C.POINTER(_i32), C.POINTER(_i32)]),
     "gm_sampler_set_layout": (_ip, [_vp, _i32, _i32]),

@@ -655,12 +655,7 @@ template <class T, int LPC, int E> struct GaussLane {
     bool done = false;
     if constexpr (GaussT<T>::template mfma_form<LPC, E>()) {
       if (mf && __builtin_amdgcn_read_exec() == ~0ull) {
-#ifdef GM_KO_PROD  // measurement build only: no product (w = d, a standard normal target)
-#pragma unroll
-        for (int e = 0; e < E; ++e) w[e] = d[e];
-#else
         mfma_product(d, w);
-#endif
         done = true;
       }
     }

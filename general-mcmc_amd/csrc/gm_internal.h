@@ -123,4 +123,9 @@ hipError_t launch_copy16(const void* src, void* dst, long long words, hipStream_
 hipError_t launch_transpose_samples(gm_dtype dt, const void* src, void* dst, long long rows,
                                     long long C, long long D, hipStream_t st);
 
+// roctx ranges when GMCMC_ROCTX=1 and the roctx library can be opened
+// (gmcmc_api.cpp); push returns whether a range was opened
+bool roctx_push(const char* name);
+void roctx_pop();
+
 }  // namespace gm

@@ -410,6 +410,20 @@ __device__ __forceinline__ u32x4 draw_block(const PhiloxKeys& K, uint32_t chain,
   }
   return c;
 }
+// The same block with the round keys re-derived by scalar adds inside the
+// call: the seed is made opaque first, so the compiler cannot hoist the 20
+// loop-invariant round keys out of a sampler's loop. In the register-heavy
+// NUTS kernel those hoisted keys were spilled to VGPR lanes and restored by a
+// v_readlane (plus its wait state) at every use; two SGPRs and ten s_add
+// pairs replace them.
+__device__ __forceinline__ u32x4 draw_block_s(uint64_t seed, uint32_t chain, uint64_t blk, uint32_t tag,
+                                              uint32_t idx) {
+  uint32_t k0 = __builtin_amdgcn_readfirstlane((uint32_t)seed);  // (uniform: a no-op where it is in SGPRs)
+  uint32_t k1 = __builtin_amdgcn_readfirstlane((uint32_t)(seed >> 32));
+  asm volatile("" : "+s"(k0), "+s"(k1));
+  u32x4 c{idx, chain, (uint32_t)blk, tag | ((uint32_t)(blk >> 32) << 8)};
+  return philox(c, k0, k1);
+}
 #endif
 
 // ---- NUTS per-transition draws (stream spec v3) ----------------------------
@@ -538,7 +552,9 @@ __device__ __forceinline__ void normals_tab(u32x4 x, double (&z)[2], const BmLds
   const double l1 = __builtin_fma(r * r, p, r);
   const double de = (double)e;
   const double lnu = __builtin_fma(de, 0x1.62e42fefa39efp-1, __builtin_fma(de, 0x1.abc9e3b39803fp-56, lc.y + l1));
-  const double rad = gsqrt(-2.0 * lnu);
+  // clamped at +0: for u1 = 1 (probability 2^-53) ln u1 rounds to +1.6e-17
+  const double m2l = -2.0 * lnu;
+  const double rad = gsqrt(m2l > 0.0 ? m2l : 0.0);
   // sin / cos of 2 pi u2
   const double u2 = Unif<double>::co(x.z, x.w);
   const int j = (int)(u2 * 256.0);
@@ -567,6 +583,17 @@ template <class T> struct NormalCache {
     }
     return pick(z, (int)(step % Blk<T>::S));
   }
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+  // get() with draw_block_s (scalar round keys; the NUTS momenta)
+  __device__ T get_s(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+    const uint64_t b = step / Blk<T>::S;
+    if (b != blk) {
+      normals_of(draw_block_s(seed, chain, b, tag, idx), z);
+      blk = b;
+    }
+    return pick(z, (int)(step % Blk<T>::S));
+  }
+#endif
 };
 template <class T> struct UniformCache {
   T u[Blk<T>::S];

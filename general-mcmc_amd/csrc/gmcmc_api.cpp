@@ -22,7 +22,7 @@
 #include <thread>
 #include <vector>
 
-#include <rocprofiler-sdk-roctx/roctx.h>
+#include <dlfcn.h>
 
 #include "gm_jit.h"
 #include "gm_layouts.h"
@@ -125,21 +125,45 @@ enum SamplerKind { K_HMC = 1, K_MH = 2, K_NUTS = 3 };
 // roctx ranges around the sampler entry points (the
 // reference times its runs with dev_tools::Timer, here the ranges appear in
 // rocprofv3 --marker-trace timelines). Enabled by GMCMC_ROCTX=1 (read once),
-// so that the bench's timed call carries no annotation cost by default.
-static bool roctx_on() {
-  static const bool on = [] {
+// so that the bench's timed call carries no annotation cost by default; the
+// roctx library is then opened with dlopen, so libgmcmc.so loads on machines
+// without rocprofiler-sdk (and the ranges are silently off there).
+namespace gm {
+struct RoctxFns {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+};
+static const RoctxFns& roctx_fns() {
+  static const RoctxFns f = [] {
+    RoctxFns r;
     const char* e = std::getenv("GMCMC_ROCTX");
-    return e && e[0] == '1';
+    if (!(e && e[0] == '1')) return r;
+    void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librocprofiler-sdk-roctx.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return r;
+    r.push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+    r.pop = (int (*)())dlsym(h, "roctxRangePop");
+    if (!r.push || !r.pop) r.push = nullptr, r.pop = nullptr;
+    return r;
   }();
-  return on;
+  return f;
 }
+bool roctx_push(const char* name) {
+  const RoctxFns& f = roctx_fns();
+  if (!f.push) return false;
+  f.push(name);
+  return true;
+}
+void roctx_pop() {
+  const RoctxFns& f = roctx_fns();
+  if (f.pop) f.pop();
+}
+}  // namespace gm
 struct RoctxRange {
   bool on;
-  explicit RoctxRange(const char* name) : on(roctx_on()) {
-    if (on) roctxRangePushA(name);
-  }
+  explicit RoctxRange(const char* name) : on(gm::roctx_push(name)) {}
   ~RoctxRange() {
-    if (on) roctxRangePop();
+    if (on) gm::roctx_pop();
   }
 };
 
@@ -1148,6 +1172,23 @@ int gm_nuts_set_lds_levels(gm_sampler* s, int32_t levels) {
   GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");
   GM_REQ(levels >= -1 && levels <= NUTS_MAX_DEPTH_LIMIT, "levels must be -1 (automatic) or 0..30");
   s->nuts.lds_levels_cap = levels;
+  return GM_OK;
+}
+
+int gm_nuts_set_dense_forms(gm_sampler* s, int32_t minv_lds, int32_t chol_lds) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");
+  GM_REQ(minv_lds >= -1 && minv_lds <= 2, "minv_lds must be -1 (automatic), 0, 1 or 2");
+  GM_REQ(chol_lds == 0 || chol_lds == 1, "chol_lds must be 0 or 1");
+  s->nuts.dense_minv_lds = minv_lds < 0 ? 2 : minv_lds;
+  s->nuts.dense_chol_lds = chol_lds;
+  return GM_OK;
+}
+
+int gm_nuts_get_plan(gm_sampler* s, int32_t* plan) {
+  GM_REQ(s && plan, "NULL argument");
+  GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");
+  for (int i = 0; i < 5; ++i) plan[i] = s->nuts.plan[i];
   return GM_OK;
 }
 

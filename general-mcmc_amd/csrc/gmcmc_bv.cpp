@@ -61,9 +61,18 @@ int gm_memcpy_dtod(void* dst, const void* src, size_t bytes) {
   if (bytes == 0) return GM_OK;
   BV_REQ(dst && src, "NULL pointer");
   // 16-byte aligned buffers of a whole number of 16-byte words (the
-  // allocator's buffers): the engine's own copy kernel; otherwise the runtime
-  if ((((uintptr_t)dst | (uintptr_t)src | (uintptr_t)bytes) & 15) == 0)
-    return bv_status(launch_copy16(src, dst, (long long)(bytes / 16), nullptr), "copy16");
+  // allocator's buffers), both on the calling thread's current device: the
+  // engine's own copy kernel; otherwise (another device, host memory,
+  // unaligned) the runtime, which also handles cross-device copies
+  if ((((uintptr_t)dst | (uintptr_t)src | (uintptr_t)bytes) & 15) == 0) {
+    int dev = -1;
+    hipPointerAttribute_t as{}, ad{};
+    if (hipGetDevice(&dev) == hipSuccess && hipPointerGetAttributes(&as, src) == hipSuccess &&
+        hipPointerGetAttributes(&ad, dst) == hipSuccess && as.type == hipMemoryTypeDevice &&
+        ad.type == hipMemoryTypeDevice && as.device == dev && ad.device == dev)
+      return bv_status(launch_copy16(src, dst, (long long)(bytes / 16), nullptr), "copy16");
+    (void)hipGetLastError();  // a failed attribute query leaves no sticky error
+  }
   return bv_status(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, nullptr), "hipMemcpy D2D");
 }
 

@@ -12,7 +12,6 @@
 #include <string>
 #include <vector>
 
-#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "gm_diag.h"
 
@@ -89,17 +88,12 @@ struct gm_comm {
 static int local_diag(const void* dev_sample, gm_dtype dtype, int64_t C, int64_t N, int64_t P,
                       int64_t sc, int64_t sd, int64_t sp, gm_comm* comm, float* rhat_out,
                       float* ess_out, hipStream_t st) {
-  static const bool rtx = [] {  // GMCMC_ROCTX=1: a roctx range per diagnostic call
-    const char* e = std::getenv("GMCMC_ROCTX");
-    return e && e[0] == '1';
-  }();
-  struct R {
+  struct R {  // GMCMC_ROCTX=1: a roctx range per diagnostic call (gm::roctx_push)
     bool on;
     ~R() {
-      if (on) roctxRangePop();
+      if (on) gm::roctx_pop();
     }
-  } rr{rtx};
-  if (rtx) roctxRangePushA(comm ? "gm_split_rhat_ess_dist" : "gm_split_rhat_ess");
+  } rr{gm::roctx_push(comm ? "gm_split_rhat_ess_dist" : "gm_split_rhat_ess")};
   GM_REQ(dtype == GM_F32 || dtype == GM_F64, "bad dtype");
   GM_REQ(C >= 1 && N >= 2 && P >= 1, "need n_chains >= 1, n_draws >= 2, n_params >= 1");
   GM_REQ(dev_sample && rhat_out && ess_out, "NULL argument");

@@ -60,11 +60,11 @@ __host__ __device__ constexpr int tri_n(int i) { return i * (i + 1) / 2; }
 template <int LPC, int E, class T> __host__ __device__ constexpr size_t minv_packed_bytes() {
   return (size_t)tri_n(LPC * E) * sizeof(T);
 }
-template <int K> __device__ __forceinline__ double row_bcast(double v) {  // lane K of the 16-lane row
-  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, 0x150 + K, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), 0x150 + K, 0xf, 0xf, false);
-  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+// lane K of the 16-lane row: one v_mov_b64_dpp (row_newbcast is the one DPP
+// control gfx950's 64-bit DPP moves take; every lane has a source, so the
+// old value is never read)
+template <int K> __device__ __forceinline__ double row_bcast(double v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + K, 0xf, 0xf, false);
 }
 template <int K> __device__ __forceinline__ float row_bcast(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x150 + K, 0xf, 0xf,
@@ -525,6 +525,25 @@ template <class T> __device__ __forceinline__ T rust_min1(T x) {  // T::one().mi
   return (x != x) ? (T)1 : (x < (T)1 ? x : (T)1);
 }
 
+// u < RN(a / b) for exact non-negative integers a <= b (b >= 1) held in T
+// and a draw u = k 2^-P (k < 2^P; P = 53 for double, 24 for float: nuts_u),
+// without the IEEE division on the common path. w = RN(u b) is within
+// 2^-P u b of the exact product, so when d = w - a is farther than a 2^-(P-4)
+// from 0 its sign is that of u b - a, i.e. of u - a/b; and then u and a/b lie
+// on the same side of RN(a/b) too (|RN(a/b) - a/b| <= 2^-P a/b), so
+// u < RN(a/b) exactly when d < 0. Inside that band (u within ~2^-(P-5)
+// relative of a/b, or a = 0 with u b tiny) the quotient itself decides, in a
+// branch that a wave takes about once per 2^15 merges. Bitwise the
+// decision u < (T)a / (T)b (generic_nuts.rs:1305-1306, 860-861).
+template <class T> __device__ __forceinline__ bool draw_below_ratio(T u, T a, T b) {
+  constexpr T rel = sizeof(T) == 8 ? (T)0x1p-49 : (T)0x1p-20f;
+  const T d = u * b - a;
+  const T m = a * rel;
+  if (__builtin_expect(d < -m, 1)) return true;
+  if (__builtin_expect(d > m, 1)) return false;
+  return u < a / b;
+}
+
 template <class T> struct MachEps;
 template <> struct MachEps<float> { static constexpr float v = 1.1920928955078125e-07f; };
 template <> struct MachEps<double> { static constexpr double v = 2.220446049250313e-16; };
@@ -600,11 +619,16 @@ constexpr int NPROF_WAVES = 8192;
 __device__ unsigned long long gm_nuts_prof_buf[NPROF_WAVES * NPROF_SLOTS];
 #endif
 
-// Launch bound: 2 blocks (2 waves per SIMD) per CU, 256 registers per lane;
-// the dense-metric instantiation 1 (512: at 256 it spilled ~500 B per lane to
-// scratch inside the loop, measured 2.1e8 leapfrogs/s at cfg3).
+// Launch bound: 2 blocks (2 waves per SIMD) per CU, 256 registers per lane,
+// for the layouts of at most 2 coordinates per lane (cfg3's 16x2 measured
+// fastest there, profiles/r03/ab/nuts_layouts.jsonl); 1 (512 registers) for
+// the dense-metric instantiation (at 256 it spilled ~500 B per lane to
+// scratch inside the loop, measured 2.1e8 leapfrogs/s at cfg3) and for
+// E >= 4, whose dozen per-lane state arrays of E values each spill at 256
+// (tools/kernel_resources.py over the build's resource remarks,
+// profiles/r04/nuts_resources.txt).
 template <class T, int LPC, int E, class TG, int MASS>
-__global__ __launch_bounds__(256, MASS == 2 ? 1 : 2) void nuts_kernel(NutsLaunch a, TG tg_) {
+__global__ __launch_bounds__(256, (MASS == 2 || E > 2) ? 1 : 2) void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
   const int lane = (int)(gtid % LPC);
@@ -891,7 +915,7 @@ __global__ __launch_bounds__(256, MASS == 2 ? 1 : 2) void nuts_kernel(NutsLaunch
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int i = lane * E + e;
-        z[e] = (i < D) ? ncache[e].get(a.seed, cid, st, TAG_NUTS_MOM, (uint32_t)i) : (T)0;
+        z[e] = (i < D) ? ncache[e].get_s(a.seed, cid, st, TAG_NUTS_MOM, (uint32_t)i) : (T)0;
       }
       momentum_from<LPC, E>(M, z, p0, lane);
     }
@@ -959,7 +983,7 @@ __global__ __launch_bounds__(256, MASS == 2 ? 1 : 2) void nuts_kernel(NutsLaunch
 #endif
       // --- transition start: slice variable, trajectory ends (:764-781)
       joint0 = lp - kin;
-      const u32x4 kw = draw_block(a.seed, cid, st, TAG_NUTS_EXP, 0u);
+      const u32x4 kw = draw_block_s(a.seed, cid, st, TAG_NUTS_EXP, 0u);
       key = nuts_key(kw);
       logu = joint0 + glog_pos(Unif<T>::oc(kw.z, kw.w));  // joint - Exp1
 #pragma unroll
@@ -983,11 +1007,7 @@ __global__ __launch_bounds__(256, MASS == 2 ? 1 : 2) void nuts_kernel(NutsLaunch
     const T joint = lp - kin;
     tn = (logu < joint) ? 1 : 0;
     ts = (logu - (T)1000) < joint;
-#ifdef GM_KO_EXP  // measurement build only: the exp skipped past warm-up (h_bar then differs)
-    ta = (a.m0 + s + 1 <= a.n_discard) ? rust_min1(gexp(joint - joint0, ek)) : (T)1;
-#else
     ta = rust_min1(gexp(joint - joint0, ek));
-#endif
     tna = 1;
 #pragma unroll
     for (int e = 0; e < E; ++e) { fq[e] = qe[e]; fp[e] = pe[e]; pr[e] = qe[e]; }
@@ -1017,19 +1037,12 @@ __global__ __launch_bounds__(256, MASS == 2 ? 1 : 2) void nuts_kernel(NutsLaunch
       int ln_, lna;
       T lal;
       stack_scalars(k, lal, ln_, lna);
-#ifdef GM_KO_MERGE  // measurement build only: no hash draw, no division
-      const double u = 0.5;
-      ++merge_ctr;
-      {
-        const bool keep_left = !(u * (double)(ln_ + tn) < (double)tn);
-#else
       const double u = nuts_u<double>(key, 64u + merge_ctr++);
       const int den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
       // (selects rather than branches from here on: the chains of a wave
       // take different sides, and a divergent branch costs both)
       {
-        const bool keep_left = !(u < (double)tn / (double)den);
-#endif
+        const bool keep_left = !draw_below_ratio(u, (double)tn, (double)den);
         T lpr[E];
         stack_vec(k, 2, lpr);
 #pragma unroll
@@ -1070,9 +1083,9 @@ __global__ __launch_bounds__(256, MASS == 2 ? 1 : 2) void nuts_kernel(NutsLaunch
     f_dbl = true;
 #endif
     {
-      const T tmp = rust_min1((T)tn / (T)n);
+      // u2 < min(1, tn / n) (:860-861): always when tn >= n (u2 < 1)
       const T u2 = nuts_u<T>(key, 2u * (uint32_t)j + 1u);
-      const bool move = ts && (u2 < tmp);
+      const bool move = ts && (tn >= n || draw_below_ratio(u2, (T)tn, (T)n));
 #pragma unroll
       for (int e = 0; e < E; ++e) q[e] = move ? pr[e] : q[e];
       acc += move ? 1 : 0;

@@ -399,15 +399,11 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
   uint64_t refind_step = 0;
   NutsLdsBudget budget;
   budget.lds_cap = ns.lds_levels_cap;  // gm_nuts_set_lds_levels (-1: as many as fit)
-  {
-    // dense M^-1 resident in LDS (layout 16 x 2) when it fits: full matrices
-    // or packed lower triangles (nuts_size_lds); GMCMC_NUTS_MINV_LDS=1 packed
-    // only, 0 global memory (A/B switches; identical results)
-    const char* e = std::getenv("GMCMC_NUTS_MINV_LDS");
-    budget.minv_lds = (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : 2;
-    const char* e2 = std::getenv("GMCMC_NUTS_CHOL_LDS");
-    budget.chol_lds = (e2 && e2[0] == '0') ? 0 : 1;
-  }
+  // dense M^-1 resident in LDS (layout 16 x 2) when it fits: full matrices
+  // or packed lower triangles (nuts_size_lds); gm_nuts_set_dense_forms picks
+  // packed only or global memory (identical results)
+  budget.minv_lds = ns.dense_minv_lds;
+  budget.chol_lds = ns.dense_chol_lds;
   {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -500,15 +496,11 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     } else {
       e = nuts_launch_layout(dt, tg, lay, a, st, budget);
     }
-    {
-      static const bool dbg = [] {  // GMCMC_NUTS_DEBUG=1: the LDS plan of each launch on stderr
-        const char* v = std::getenv("GMCMC_NUTS_DEBUG");
-        return v && v[0] == '1';
-      }();
-      if (dbg)
-        fprintf(stderr, "gmcmc nuts launch: lds_max %d ncu %d stack levels in LDS %d, M^-1 in LDS %d at %u, L %d at %u\n",
-                budget.lds_max, budget.ncu, a.lds_levels, a.minv_lds, a.minv_lds_off, a.chol_lds, a.chol_lds_off);
-    }
+    ns.plan[0] = a.lds_levels;  // gm_nuts_get_plan
+    ns.plan[1] = a.minv_lds;
+    ns.plan[2] = (int)a.minv_lds_off;
+    ns.plan[3] = a.chol_lds;
+    ns.plan[4] = (int)a.chol_lds_off;
     if (e != hipSuccess) {
       set_error(std::string("NUTS launch failed: ") + hipGetErrorString(e));
       return GM_EHIP;

@@ -18,8 +18,8 @@ struct NutsLdsBudget {
   int lds_max = 64 * 1024;      // dynamic LDS per block
   long long lds_cap = -1;       // levels cap (-1: as many as fit)
   int minv_lds = 2;             // dense metric in LDS when it fits: 2 full or packed, 1 packed only, 0 off
-                                // (GMCMC_NUTS_MINV_LDS)
-  int chol_lds = 1;             // its Cholesky factor too (GMCMC_NUTS_CHOL_LDS=0: off)
+                                // (gm_nuts_set_dense_forms)
+  int chol_lds = 1;             // its Cholesky factor too (0: off)
 };
 
 // LDS of a launch: the target's staging area (tgl bytes), then as many

@@ -103,6 +103,20 @@ class NUTS(Sampler):
         _lib.check(self._lib.gm_nuts_set_lds_levels(self._h, int(levels)))
         return self
 
+    def set_dense_forms(self, minv_lds: int = -1, chol_lds: int = 1):
+        """Placement of the dense metric's matrices (gm_nuts_set_dense_forms):
+        minv_lds 2/-1 full-or-packed in LDS, 1 packed only, 0 global memory;
+        chol_lds 1 the packed Cholesky factor in LDS too. Identical results."""
+        _lib.check(self._lib.gm_nuts_set_dense_forms(self._h, int(minv_lds), int(chol_lds)))
+        return self
+
+    def launch_plan(self) -> dict:
+        """The last launch's on-chip plan (gm_nuts_get_plan)."""
+        p = np.zeros(5, dtype=np.int32)
+        _lib.check(self._lib.gm_nuts_get_plan(self._h, _lib.ptr(p)))
+        return {"lds_levels": int(p[0]), "minv_lds": int(p[1]), "minv_off": int(p[2]), "chol_lds": int(p[3]),
+                "chol_off": int(p[4])}
+
     def step_sizes(self) -> tuple[np.ndarray, np.ndarray]:
         """Per-chain (epsilon, epsilon_bar)."""
         eps = np.empty(self.n_chains, dtype=np.float64)

@@ -231,6 +231,20 @@ int gm_nuts_set_mass_adaptation(gm_sampler* s, int32_t mode, int64_t start_buffe
  * target's staging area. Results are identical for every value. */
 int gm_nuts_set_lds_levels(gm_sampler* s, int32_t levels);
 
+/* Where a dense-metric NUTS sampler (layout 16 x 2, dim <= 32) keeps each
+ * chain's M^-1 and Cholesky factor: minv_lds 2 (the default, also -1) the
+ * full matrices in LDS when they fit next to the target's staging, else the
+ * packed lower triangles; 1 packed triangles only; 0 global memory.
+ * chol_lds 1 also packs the Cholesky factor into LDS when the packed M^-1
+ * leaves room. Every form gives identical results (no reference
+ * counterpart: a placement choice of this engine). */
+int gm_nuts_set_dense_forms(gm_sampler* s, int32_t minv_lds, int32_t chol_lds);
+
+/* The last NUTS launch's on-chip plan: plan[0] subtree-stack levels in LDS,
+ * plan[1] M^-1 form (0 global, 1 packed, 2 full), plan[2] its LDS offset,
+ * plan[3] Cholesky factor in LDS (0/1), plan[4] its offset. */
+int gm_nuts_get_plan(gm_sampler* s, int32_t* plan);
+
 int gm_nuts_get_mass(gm_sampler* s, int32_t* mode, int32_t* kind, void* dinv, void* dsqrt, void* minv,
                      void* mchol);
 

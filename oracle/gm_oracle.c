@@ -237,9 +237,10 @@ double or_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, u
 #include "gm_bm_tables.h"
 static const double bm_log[256] = {GM_BM_LOG_INIT};
 static const double bm_sincos[512] = {GM_BM_SINCOS_INIT};
-double or_tab_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
-  uint32_t x[4];
-  block(seed, chain, step / 2, tag, idx, x);
+/* The pair (z0, z1) of one block's words x. -2 ln u1 is clamped at +0: for
+ * u1 = 1 (probability 2^-53) the table form's ln rounds to +1.6e-17, and the
+ * clamp keeps that r = 0 instead of sqrt of a negative (NaN). */
+void or_tab_normal_pair(const uint32_t x[4], double z[2]) {
   const double u1 = unif_oc_d(x[0], x[1]);
   const uint64_t b = bits_d(u1);
   const int e = (int)(b >> 52) - 1023;
@@ -255,7 +256,8 @@ double or_tab_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t ta
   const double l1 = fma(r * r, p, r);
   const double de = (double)e;
   const double lnu = fma(de, 0x1.62e42fefa39efp-1, fma(de, 0x1.abc9e3b39803fp-56, logc + l1));
-  const double rad = sqrt(-2.0 * lnu);
+  const double m2l = -2.0 * lnu;
+  const double rad = sqrt(m2l > 0.0 ? m2l : 0.0);
   const double u2 = unif_co_d(x[2], x[3]);
   const int j = (int)(u2 * 256.0);
   const double th = (u2 - (double)j * 0.00390625) * 0x1.921fb54442d18p+2;
@@ -265,7 +267,15 @@ double or_tab_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t ta
   const double S = bm_sincos[2 * j], Cc = bm_sincos[2 * j + 1];
   const double sv = fma(Cc, sth, fma(S, cm, S));
   const double cv = fma(-S, sth, fma(Cc, cm, Cc));
-  return (step % 2 == 0) ? rad * cv : rad * sv;
+  z[0] = rad * cv;
+  z[1] = rad * sv;
+}
+double or_tab_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  uint32_t x[4];
+  double z[2];
+  block(seed, chain, step / 2, tag, idx, x);
+  or_tab_normal_pair(x, z);
+  return z[step % 2];
 }
 float or_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
 static float or_mh_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {

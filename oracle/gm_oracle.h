@@ -53,6 +53,7 @@ float or_cos2pi_f(float u);
 double or_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
 float or_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
 /* the f64 MH proposal normal (spec v5: table-driven Box-Muller) */
+void or_tab_normal_pair(const uint32_t x[4], double z[2]);
 double or_tab_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
 double or_uniform_co_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
 float or_uniform_co_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);

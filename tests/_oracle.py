@@ -51,6 +51,8 @@ def load():
         if sfx == "d":
             lib.or_tab_normal_d.restype = rt
             lib.or_tab_normal_d.argtypes = [_u64, _u32, _u64, _u32, _u32]
+            lib.or_tab_normal_pair.restype = None
+            lib.or_tab_normal_pair.argtypes = [_vp, _vp]
         getattr(lib, f"or_uniform_co_{sfx}").restype = rt
         getattr(lib, f"or_uniform_co_{sfx}").argtypes = [_u64, _u32, _u64, _u32, _u32]
         getattr(lib, f"or_logp_grad_{sfx}").restype = rt

@@ -11,7 +11,7 @@ import numpy as np
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ARGV = ["--steps", "8", "--warmup", "2", "--chains", "128", "--cpu-seconds", "0.05",
+ARGV = ["--steps", "8", "--warmup", "2", "--chains", "128", "--cpu-seconds", "0.05", "--cpu-config-seconds", "0.05",
         "--ess-discard", "4", "--ess-collect", "8", "--ess-long-discard", "4", "--ess-long-collect", "8"]
 
 
@@ -205,3 +205,10 @@ def test_bench_line_world1_and_world2(tmp_path):
         assert c5["value"] == 16384 * world * 1100 / (0.1 * world)
         assert c5["roofline"]["hbm_equivalent"]["frac"] > 0
         assert line["configs"]["cfg4"]["transitions"] == 200
+        # a CPU baseline beside every config leg, at all cores and at 1 thread
+        for name, unit in (("cfg3", "leapfrog steps/s (sampling phase)"),
+                           ("cfg3_dense", "leapfrog steps/s (whole run, dense warm-up included)"),
+                           ("cfg4", "chain-leapfrog steps/s"), ("cfg5", "chain-steps/s")):
+            cb = line["configs"][name]["cpu_baseline"]
+            assert cb["unit"] == unit and cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+            assert cb["one_thread"]["cores"] == 1 and cb["one_thread"]["value"] > 0

@@ -19,11 +19,15 @@ def _gauss(gm, cov, mean=None):
     return gm.DenseGaussian(mean, cov)
 
 
-def _check_run(gm, oracle, t, x0, dtype, mode, runs, progress=False, **cfg):
+def _check_run(gm, oracle, t, x0, dtype, mode, runs, progress=False, layout=None, forms=None, **cfg):
     C_, D = x0.shape
     adapt = {1: "diagonal", 2: "dense"}[mode]
     mc = gm.NUTSMassMatrixConfig(adapt, **{**dict(regularize=0.05, jitter=1e-6, dense_max_dim=75), **cfg})
     s = gm.NUTS.new_with_mass_matrix(t, x0, 0.8, mc, dtype=dtype).set_seed(11)
+    if layout:
+        s.set_layout(*layout)
+    if forms:
+        s.set_dense_forms(**forms)
     lanes, elems = s.layout()
     ot = Target.from_product(t, D)
     st = oracle.nuts_state(C_, dtype)
@@ -85,25 +89,29 @@ def test_dense_warmup_wide_layout(gm, oracle):
 
 @pytest.mark.parametrize("minv_lds,chol_lds", [("2", "1"), ("1", "1"), ("1", "0"), ("0", "0")])
 @pytest.mark.parametrize("D,chains", [(20, 10), (32, 36)])
-def test_dense_warmup_matrix_core_layout(gm, oracle, monkeypatch, minv_lds, chol_lds, D, chains):
-    """f64 at 16 lanes x 2 (the dense Gaussian's product on the matrix cores)
-    with each form of the dense metric's products: M^-1 full in LDS (2), its
-    packed lower triangle with or without the packed Cholesky factor (1), and
-    the transposed per-chain matrices in global memory (0)
-    (GMCMC_NUTS_MINV_LDS / GMCMC_NUTS_CHOL_LDS, nuts_launch.h); D = 20 pads
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_dense_warmup_matrix_core_layout(gm, oracle, minv_lds, chol_lds, D, chains, dtype):
+    """f64 and f32 at 16 lanes x 2 (the dense Gaussian's layout; its product
+    on the matrix cores for f64) with each form of the dense metric's
+    products: M^-1 full in LDS (2), its packed lower triangle with or without
+    the packed Cholesky factor (1), and the transposed per-chain matrices in
+    global memory (0) (gm_nuts_set_dense_forms, nuts_launch.h); D = 20 pads
     rows and columns to 32, and 10 or 36 chains leave the last wave partly
-    empty (the VALU target product there)."""
-    monkeypatch.setenv("GMCMC_NUTS_MINV_LDS", minv_lds)
-    monkeypatch.setenv("GMCMC_NUTS_CHOL_LDS", chol_lds)
+    empty (the VALU target product there). The launch plan read back shows
+    the form actually used."""
     rng = np.random.default_rng(21)
     a = rng.standard_normal((D, D))
     cov = a @ a.T / D + 0.5 * np.eye(D)
     t = _gauss(gm, cov, rng.standard_normal(D))
-    x0 = gm.init_with_seed(chains, D, 6, np.float64)
-    s, om = _check_run(gm, oracle, t, x0, np.float64, 2, [(8, 45), (6, 20)], start_buffer=4, end_buffer=4,
-                       initial_window=10)
+    x0 = gm.init_with_seed(chains, D, 6, np.float64).astype(dtype)
+    forms = dict(minv_lds=int(minv_lds), chol_lds=int(chol_lds))
+    s, om = _check_run(gm, oracle, t, x0, dtype, 2, [(8, 45), (6, 20)], start_buffer=4, end_buffer=4,
+                       initial_window=10, layout=(16, 2), forms=forms)
     assert s.layout() == (16, 2)
     assert np.any(om.kind == 2)
+    plan = s.launch_plan()
+    assert plan["minv_lds"] == int(minv_lds) or (minv_lds == "2" and plan["minv_lds"] == 1)
+    assert plan["chol_lds"] <= int(chol_lds) and (plan["chol_lds"] == 0 or plan["minv_lds"] == 1)
 
 
 def test_progress_semantics_with_mass(gm, oracle):
@@ -143,3 +151,42 @@ def test_default_schedule_recovers_scales(gm, oracle):
                                             50, 600, False, lanes, elems, chain_offset=c)
         np.testing.assert_array_equal(out[c], smp[:, 0, :])
         np.testing.assert_array_equal(m.diag_inv[c], om.dinv[0])
+
+
+def test_dense_metric_convention_is_reference_M_equals_cov(gm):
+    """The reference's metric convention, pinned on cfg3's target. Its dense
+    warm-up sets the MASS matrix to the regularised sample covariance,
+    M = C = 0.95 Sigma_hat + 0.05 I (generic_nuts.rs:975-989): dense_from_cov
+    keeps inv = C^-1 for the kinetic energy and drift and chol = cholesky(C)
+    for the momentum, p = chol z ~ N(0, C) (:209-224, 255-303). Stan's
+    convention is the inverse (M^-1 = C): the reference's drift M^-1 p then
+    rescales the target's directions by Sigma^-1 instead of Sigma, which is
+    why cfg3 with dense adaptation mixes worse than with the identity metric
+    (bench cfg3_dense). The engine reproduces the reference:
+      * mean over chains of inv(dense_inv) is C to 15 % (Frobenius, relative;
+        each chain's last window holds ~200 draws, 512 chains);
+      * dense_inv is C^-1 (to 50 %: the mean of inverted estimates is biased
+        up by ~n/(n-D-1)), not Stan's C (1.2 away, relative);
+      * chol chol^T = inv(dense_inv) per chain (to 1e-9 relative)."""
+    rng = np.random.default_rng(42)
+    q, _ = np.linalg.qr(rng.standard_normal((32, 32)))
+    cov = q @ np.diag(np.logspace(-1, 1, 32)) @ q.T
+    cov = 0.5 * (cov + cov.T)
+    t = gm.DenseGaussian(np.zeros(32), cov)
+    s = gm.NUTS.new_with_mass_matrix(t, gm.init_det(512, 32), 0.8, gm.NUTSMassMatrixConfig("dense"),
+                                     dtype=np.float64).set_seed(5)
+    s.run(1, 500)
+    m = s.mass_matrix()
+    assert np.all(m.kind == 2)
+    c_reg = 0.95 * cov + 0.05 * np.eye(32)
+    c_hat = np.linalg.inv(m.dense_inv)  # each chain's regularised covariance estimate
+    rel = np.linalg.norm(c_hat.mean(axis=0) - c_reg) / np.linalg.norm(c_reg)
+    assert rel < 0.15, rel
+    minv_mean = m.dense_inv.mean(axis=0)
+    inv_c = np.linalg.inv(c_reg)
+    assert np.linalg.norm(minv_mean - inv_c) / np.linalg.norm(inv_c) < 0.5
+    # Stan's convention would put C itself there: 1.2 away (relative) from C^-1 here
+    assert np.linalg.norm(minv_mean - c_reg) / np.linalg.norm(c_reg) > 0.9
+    for c in (0, 101, 511):
+        L = m.dense_chol[c]
+        np.testing.assert_allclose(L @ L.T, c_hat[c], rtol=1e-9, atol=1e-9 * np.abs(c_hat[c]).max())

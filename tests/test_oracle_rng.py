@@ -87,6 +87,21 @@ def test_tab_normal_pairs_and_moments(oracle):
     assert np.all(np.isfinite(z))
 
 
+def test_tab_normal_u1_one_is_zero(oracle):
+    """u1 = 1 (all-ones words, probability 2^-53): the table form's ln u1
+    rounds to +1.6e-17, so -2 ln u1 < 0; the clamp makes the pair exactly
+    (+0, +0) instead of NaN (the reference's Box-Muller never yields NaN)."""
+    lib = oracle.lib
+    z = np.zeros(2)
+    for w2, w3 in ((0, 0), (0x12345678, 0x9ABCDEF0), (0xFFFFFFFF, 0xFFFFFFFF)):
+        x = np.array([0xFFFFFFFF, 0xFFFFFFFF, w2, w3], dtype=np.uint32)
+        lib.or_tab_normal_pair(x.ctypes.data, z.ctypes.data)
+        assert np.all(np.isfinite(z)) and np.all(z == 0.0), (w2, w3, z)
+    x = np.array([0xFFFFFFFF, 0xFFFFFFC0 - 1, 7, 9], dtype=np.uint32)  # the next u1 below 1
+    lib.or_tab_normal_pair(x.ctypes.data, z.ctypes.data)
+    assert np.all(np.isfinite(z)) and 0 < np.hypot(*z) < 1e-7
+
+
 def test_nuts_stream_mix64_splitmix_kat(oracle):
     """The NUTS per-transition draws hash K + (idx + 1) * 0x9E3779B97F4A7C15
     with the SplitMix64 finalizer: K = 1234567 reproduces the published

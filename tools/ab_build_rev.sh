@@ -14,6 +14,6 @@ mkdir -p "$OUT" "$SRC/csrc" "$SRC/include"
 B=$ROOT/general-mcmc_amd/build
 OBJS=$(ls $B/*.o | grep -v "/$tu.o")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libgmcmc.so" "$OUT/$tu.o" $OBJS \
-  -L/opt/rocm/lib -lrccl -lhiprtc -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
+  -L/opt/rocm/lib -lrccl -lhiprtc -ldl -Wl,-rpath,/opt/rocm/lib
 rm -rf "$OUT/$tu.o" "$SRC"
 echo "built abtest/$name ($tu from $rev)"

@@ -11,5 +11,5 @@ FLAGS="$AB_DEFS --offload-arch=gfx950 -O3 -std=c++20 -ffp-contract=off -fno-slp-
 B=$ROOT/general-mcmc_amd/build
 OBJS=$(ls $B/*.o | grep -v "/$UNIT.o")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libgmcmc.so" "$OUT/$UNIT.o" $OBJS \
-  -L/opt/rocm/lib -lrccl -lhiprtc -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
+  -L/opt/rocm/lib -lrccl -lhiprtc -ldl -Wl,-rpath,/opt/rocm/lib
 rm -f "$OUT/$UNIT.o"

@@ -47,6 +47,9 @@ def cfg3(a):
         s.set_layout(*[int(v) for v in a.nuts_layout.split("x")])
     if a.nuts_lds_levels >= 0:
         s.set_lds_levels(a.nuts_lds_levels)
+    if a.nuts_dense_forms:
+        mi, ch = (int(v) for v in a.nuts_dense_forms.split(","))
+        s.set_dense_forms(mi, ch)
     # warm-up (step-size adaptation) then sampling, as NUTS::run_progress
     _, tw = timed(lambda: s.run_positions(1, a.nuts_discard))
     lf0 = s.leapfrog_counts().sum()
@@ -57,7 +60,7 @@ def cfg3(a):
     return {"config": "cfg3 NUTS DenseGaussian32 f64", "chains": C, "layout": "%dx%d" % s.layout(),
             "mass_adaptation": a.nuts_mass,
             "warmup_s": tw, "sample_s": ts, "leapfrogs": int(lf), "leapfrog_per_s": lf / ts,
-            "mean_tree_leapfrogs": lf / (C * a.nuts_collect), "eps_median": float(np.median(eps)),
+            "mean_tree_leapfrogs": lf / (C * a.nuts_collect), "plan": s.launch_plan(), "eps_median": float(np.median(eps)),
             "ess_mean": float(ess.mean()), "ess_min": float(ess.min()), "rhat_max": float(rhat.max()),
             "ess_per_s": float(ess.mean()) / ts}
 
@@ -111,6 +114,7 @@ def main():
                    help="cfg3 with the warm-up metric adaptation (new_with_mass_matrix)")
     p.add_argument("--nuts-chains", type=int, default=8192)
     p.add_argument("--nuts-lds-levels", type=int, default=-1, help="cap on the subtree-stack levels held in LDS")
+    p.add_argument("--nuts-dense-forms", default="", help="minv_lds,chol_lds (gm_nuts_set_dense_forms)")
     p.add_argument("--nuts-discard", type=int, default=500)
     p.add_argument("--nuts-collect", type=int, default=500)
     p.add_argument("--nuts-layout", default="")

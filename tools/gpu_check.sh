@@ -30,9 +30,8 @@ for step in "$@"; do
     nlevels) run nuts_levels 300 python tools/probe_nuts_levels.py ;;
     nutstest) run nuts_tests 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_mfma_gauss.py tests/test_gpu_nuts_truncation.py tests/test_gpu_nuts_mass.py tests/test_gpu_fullsize_edge.py tests/test_gpu_checkpoint.py tests/test_gpu_step.py -x -q -k "nuts or NUTS or cfg3 or mfma" --timeout 120 --timeout-method thread ;;
     masstest) run mass_tests 300 python -u -m pytest tests/test_gpu_nuts_mass.py tests/test_gpu_mfma_gauss.py tests/test_gpu_nuts_truncation.py -x -q --timeout 120 --timeout-method thread ;;
-    densemass) run dense_lds0 300 env GMCMC_NUTS_MINV_LDS=0 python tools/bench_configs.py --which 3 --nuts-mass dense &&
-               run dense_lds1 300 env GMCMC_NUTS_MINV_LDS=1 python tools/bench_configs.py --which 3 --nuts-mass dense &&
-               run dense_lds1_test 300 env GMCMC_NUTS_MINV_LDS=1 python -u -m pytest tests/test_gpu_nuts_mass.py -x -q --timeout 120 --timeout-method thread ;;
+    densemass) run dense_lds0 300 python tools/bench_configs.py --which 3 --nuts-mass dense --nuts-dense-forms 0,0 &&
+               run dense_lds1 300 python tools/bench_configs.py --which 3 --nuts-mass dense --nuts-dense-forms 1,1  ;;
     mhtest) run mh_tests 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize_edge.py tests/test_gpu_tracker.py -x -q -k "mh or MH or cfg5 or Metropolis or tracker" --timeout 120 --timeout-method thread ;;
     warmup) run warmup_probe 300 python tools/probe_warmup.py ;;
     hostpath) run host_path 120 python tools/probe_host_path.py ;;
@@ -47,6 +46,12 @@ for step in "$@"; do
       for v in ${FIRST_VARIANTS:-"--warm-collect --scratch-warm 2" "--warm-collect --scratch-warm 2" "--warm-collect --scratch-warm 2"}; do
         run first_call 60 python tools/probe_bench_first.py --repeat 4 $v && cat gpurun_out/first_call.log >> gpurun_out/first_calls.jsonl
       done ;;
+    abhd)
+      for r in 1 2; do for l in general-mcmc_amd/lib/libgmcmc.so $AB_LIBS; do
+        run nuts_highdim 300 env GMCMC_LIB=$(pwd)/$l python tools/probe_nuts_highdim.py &&
+          sed "s|^{|{\"lib\": \"$l\", |" gpurun_out/nuts_highdim.log >> gpurun_out/nuts_highdim.jsonl
+      done; done ;;
+    abdense) AB_ARGS="--nuts-mass dense" AB_ROUNDS=${AB_ROUNDS:-2} run ab_dense 900 python tools/ab_nuts.py general-mcmc_amd/lib/libgmcmc.so ${AB_LIBS} ;;
     nprof) run nuts_prof 120 env GMCMC_LIB=abtest/nprof/libgmcmc.so python tools/probe_nuts_prof.py ;;
   esac
 done

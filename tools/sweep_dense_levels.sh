@@ -3,6 +3,6 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}" && mkdir -p gpurun_out
 for cfg in "2 0" "2 1" "1 0" "1 1" "1 3" "1 6"; do
   set -- $cfg
-  r=$(GMCMC_NUTS_MINV_LDS=$1 GMCMC_NUTS_CHOL_LDS=0 timeout -k 10 200 python tools/bench_configs.py --which 3 --nuts-mass dense --nuts-lds-levels $2 | tail -1) || exit $?
+  r=$(timeout -k 10 200 python tools/bench_configs.py --which 3 --nuts-mass dense --nuts-dense-forms $1,0 --nuts-lds-levels $2 | tail -1) || exit $?
   echo "minv_lds=$1 levels<=$2 $(echo "$r" | grep -o '"leapfrog_per_s": [0-9.e+]*')"
 done
