@@ -36,7 +36,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 VALU_F32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md, spec)
 VALU_F64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (MI355X_MICROARCH.md, spec)
 METRIC = "leapfrog steps/sec (whole node) + ESS/sec, 64-dim Rosenbrock HMC at 1/2/4/8 GPUs"
-PMC_FILE = os.path.join(ROOT, "profiles", "r03", "pmc_hmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r04", "pmc_hmc.json")
+PMC_CONFIGS_FILE = os.path.join(ROOT, "profiles", "r04", "pmc_configs.json")  # tools/profile_r04.sh
 
 
 def parse(argv=None):
@@ -599,6 +600,33 @@ def rhat_block(rhat):
             "max_abs_dev_from_1": fin(np.max(np.abs(stan - 1.0)))}
 
 
+def f_alg_mh(D):
+    """Algorithmic flops of one MH chain-step on the isotropic Gaussian
+    (metropolis_hastings.rs:306-318; distributions.rs:378-406): the proposal
+    x' = x + sd z (2D), the target's sum of squares and scale (2D + 2), the
+    proposal's forward and backward log-densities (3D + 2 each). The D
+    normals and the accept uniform are RNG work, counted separately
+    (SURVEY 8(d))."""
+    return 10 * D + 6
+
+
+def load_pmc_config(name):
+    """PMC figures of a config leg's dispatch (profiles/r04/pmc_configs.json,
+    tools/profile_r04.sh), or None."""
+    try:
+        e = json.load(open(PMC_CONFIGS_FILE)).get(name)
+    except (OSError, ValueError):
+        return None
+    if not e or not e.get("by_steps"):
+        return None
+    k, r = next(iter(e["by_steps"].items()))
+    v = r.get("valu", {})
+    return {"transitions_per_launch": int(k), "launch_us_traced": r.get("launch_us_traced"),
+            "hbm_bytes_per_launch": r.get("hbm_bytes_per_launch"), "issue_frac": v.get("issue_frac"),
+            "valu_insts_per_wave": v.get("valu_insts_per_wave"), "salu_per_valu": v.get("salu_per_valu"),
+            "wave_wait_frac": v.get("wave_wait_frac"), "source": r.get("source")}
+
+
 def config_summary(name, cfg, figs, world, rhat, ess):
     """Aggregate one config leg over the ranks (max time, summed work) with
     its own roofline: the FP64/FP32 vector peak for NUTS / HMC (F_alg of
@@ -619,7 +647,11 @@ def config_summary(name, cfg, figs, world, rhat, ess):
         lf_w = sum(f.get("warmup_leapfrogs", 0) for f in figs)
         t_w = max(f.get("warmup_s", 0.0) for f in figs)
         n_samp = cfg["n_collect"] - 1
-        fa = 2 * D * D + 8 * D
+        # the target's GEMV and the kicks/drift, 2D^2 + 8D; under
+        # a dense metric each leaf adds two M^-1 products (the drift's and the
+        # kinetic energy's, generic_nuts.rs:255-273, 1396-1418), 2D^2 each (the
+        # products at doubling ends and transition starts are not counted)
+        fa = 2 * D * D + 8 * D + (4 * D * D if cfg.get("mass") == "dense" else 0)
         tf = fa * (lf / world) / (kms * 1e-3) / 1e12
         mass = f", {cfg['mass']} mass-matrix adaptation" if cfg.get("mass") else ""
         out.update(workload=f"NUTS DenseGaussian dim={D} f64, {chains} chains, target_accept "
@@ -635,7 +667,8 @@ def config_summary(name, cfg, figs, world, rhat, ess):
                    roofline={"bound": "valu_f64", "kernel": "nuts_kernel", "achieved": tf,
                              "peak": VALU_F64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / VALU_F64_PEAK_TFLOPS,
                              "flops_per_leapfrog": fa,
-                             "note": "F = 2D^2 + 8D per leapfrog (SURVEY 8(d)) x leapfrogs counted on the "
+                             "note": "F = 2D^2 + 8D per leapfrog (SURVEY 8(d)), + 4D^2 for the two M^-1 "
+                                     "products of a leaf under a dense metric, x leapfrogs counted on the "
                                      "device / the run's HIP-event kernel time (per GPU)"})
     elif cfg["kind"] == "hmc":
         work = chains * cfg["L"] * total
@@ -650,15 +683,26 @@ def config_summary(name, cfg, figs, world, rhat, ess):
         work = chains * total
         b = (2 * D + 2) * s_bytes
         gbs = b * (work / world) / (kms * 1e-3) / 1e9
+        fa = f_alg_mh(D)
+        tf = fa * (work / world) / (kms * 1e-3) / 1e12
         out.update(workload=f"MH IsotropicGaussian(1) dim={D} f64, proposal sd {cfg['proposal_std']:.5f}, "
                             f"{chains} chains, run({cfg['n_collect']}, {cfg['n_discard']})",
                    metric="chain-steps/s", value=work / t, value_kernel=work / (kms * 1e-3),
-                   roofline={"bound": "valu", "kernel": "mh_kernel",
+                   roofline={"bound": "valu_f64", "kernel": "mh_kernel", "achieved": tf,
+                             "peak": VALU_F64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / VALU_F64_PEAK_TFLOPS,
+                             "flops_per_chain_step": fa,
+                             "rng_normals_per_s": D * (work / world) / (kms * 1e-3),
                              "hbm_equivalent": {"achieved_gbs": gbs, "peak_gbs": HBM_PEAK_GBS,
                                                 "frac": gbs / HBM_PEAK_GBS, "bytes_per_chain_step": b},
-                             "note": "per coordinate-step one f64 Philox/Box-Muller normal and one IEEE "
-                                     "divide: VALU-bound; the HBM-equivalent is SURVEY 8(d)'s (2D+2)s bytes "
-                                     "per chain-step over the kernel time (per GPU)"})
+                             "note": "achieved = F_alg (10D+6 per chain-step: proposal, target and the two "
+                                     "proposal log-densities, f_alg_mh) x chain-steps / the run's HIP-event "
+                                     "kernel time (per GPU), against the FP64 vector peak. The D Philox/"
+                                     "Box-Muller normals per chain-step are RNG work outside F_alg (SURVEY "
+                                     "8(d)) and take most of the VALU issue (pmc.issue_frac); the "
+                                     "HBM-equivalent is SURVEY 8(d)'s (2D+2)s bytes per chain-step"})
+    pm = load_pmc_config(name)
+    if pm is not None:
+        out["roofline"]["pmc"] = pm
     out["ess_mean"] = fin(np.mean(ess))
     out["ess_min"] = fin(np.min(ess))
     out["ess_per_sec"] = fin(np.mean(ess) / t)

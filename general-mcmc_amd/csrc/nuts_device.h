@@ -186,46 +186,6 @@ __device__ __forceinline__ void chol_global_cols(const T* const (&pb)[E], int D,
   }
 }
 
-// full_cols software-pipelined (GM_FULL_PIPE = batch width): batch J + NB's
-// reads and broadcasts are issued before batch J's sums, so the LDS latency
-// of all but the first batch hides behind the dependent adds. Same sums.
-template <int LPC, int E, class T, int J, int NB>
-__device__ __forceinline__ void full_cols_load(unsigned base, const T (&p)[E],
-                                               T (&m)[NB][E], T (&pj)[NB]) {
-  constexpr int DP = LPC * E;
-  typedef T vE __attribute__((ext_vector_type(E)));
-#pragma unroll
-  for (int u = 0; u < NB; ++u) {
-    const vE w = *(const vE*)(gm_dyn_lds + base + (J + u) * DP * sizeof(T));
-#pragma unroll
-    for (int e = 0; e < E; ++e) m[u][e] = w[e];
-  }
-  row_bcasts<E, T, J, 0, NB>(p, pj);
-}
-template <int LPC, int E, class T, int J, int NB>
-__device__ __forceinline__ void full_cols_pipe(unsigned base, const T (&p)[E], const T (&m)[NB][E],
-                                               const T (&pj)[NB], T (&acc)[E]) {
-  constexpr int DP = LPC * E;
-  if constexpr (J + NB < DP) {
-    T m2[NB][E], pj2[NB];
-    full_cols_load<LPC, E, T, J + NB, NB>(base, p, m2, pj2);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < NB; ++u) {
-#pragma unroll
-      for (int e = 0; e < E; ++e) acc[e] = acc[e] + m[u][e] * pj[u];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    full_cols_pipe<LPC, E, T, J + NB, NB>(base, p, m2, pj2, acc);
-  } else {
-#pragma unroll
-    for (int u = 0; u < NB; ++u) {
-#pragma unroll
-      for (int e = 0; e < E; ++e) acc[e] = acc[e] + m[u][e] * pj[u];
-    }
-  }
-}
-
 // columns per batch of the dense products (their loads / broadcasts issued
 // together; the sums stay in ascending j). 4 keeps the dense-metric kernel
 // within 256 registers (2 waves per SIMD; 8 took it to 276 and 1 wave).
@@ -245,15 +205,10 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E, K>& M, const T (&p)[
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
     if constexpr (LPC == 16 && E == 2) {
       if (M.minv_lds == 2) {
-#ifdef GM_FULL_PIPE
-        static_assert((LPC * E) % GM_FULL_PIPE == 0, "batch width divides the padded dimension");
-        T m0[GM_FULL_PIPE][E], pj0[GM_FULL_PIPE];
-        const unsigned base = M.lds_off + (unsigned)(lane * E * (int)sizeof(T));
-        full_cols_load<LPC, E, T, 0, GM_FULL_PIPE>(base, p, m0, pj0);
-        full_cols_pipe<LPC, E, T, 0, GM_FULL_PIPE>(base, p, m0, pj0, acc);
-#else
+        // (software-pipelining the batches, batch J+1's reads and broadcasts
+        // issued before batch J's sums, measured -1 % / -5 % at 4 / 8
+        // columns per batch, profiles/r04/ab_dense_pipe.log: not kept)
         full_cols<LPC, E, T, 0>(M.lds_off + (unsigned)(lane * E * (int)sizeof(T)), p, acc);
-#endif
 #pragma unroll
         for (int e = 0; e < E; ++e) v[e] = acc[e];
         return;
@@ -499,6 +454,8 @@ __device__ __forceinline__ bool no_uturn_m(const MassDev<T, E, K>& M, const T (&
   T d[E], vm[E], vp[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) d[e] = qp[e] - qm[e];
+  // (the two products fused, one LDS read of each column for both: -2 %,
+  // profiles/r04/ab_dense_uturn_pair.log, not kept)
   inv_mul<LPC, E>(M, pm, vm, lane);
   inv_mul<LPC, E>(M, pp, vp, lane);
   const T dm = dot_group<LPC, E>(d, vm);
@@ -620,15 +577,19 @@ __device__ unsigned long long gm_nuts_prof_buf[NPROF_WAVES * NPROF_SLOTS];
 #endif
 
 // Launch bound: 2 blocks (2 waves per SIMD) per CU, 256 registers per lane,
-// for the layouts of at most 2 coordinates per lane (cfg3's 16x2 measured
+// for up to 8 f32 or 2 f64 coordinates per lane (cfg3's 16x2 measured
 // fastest there, profiles/r03/ab/nuts_layouts.jsonl); 1 (512 registers) for
 // the dense-metric instantiation (at 256 it spilled ~500 B per lane to
 // scratch inside the loop, measured 2.1e8 leapfrogs/s at cfg3) and for
-// E >= 4, whose dozen per-lane state arrays of E values each spill at 256
-// (tools/kernel_resources.py over the build's resource remarks,
-// profiles/r04/nuts_resources.txt).
+// wider lanes, whose dozen per-lane state arrays of E values each spill at
+// 256 (tools/kernel_resources.py over the build's resource remarks,
+// profiles/r04/nuts_resources.txt). Measured at 2048 chains, IsotropicGaussian
+// (tools/probe_nuts_highdim.py, profiles/r04/nuts_highdim.jsonl): 1 wave per
+// SIMD f64 64x4 +4 %, 64x8 +78 %, 64x16 +150 %, f32 64x16 +55 %, but f32
+// 64x4 -6 % and 64x8 -4 %, which therefore keep 2.
 template <class T, int LPC, int E, class TG, int MASS>
-__global__ __launch_bounds__(256, (MASS == 2 || E > 2) ? 1 : 2) void nuts_kernel(NutsLaunch a, TG tg_) {
+__global__ __launch_bounds__(256, (MASS == 2 || E * (int)sizeof(T) > 32 || (sizeof(T) == 8 && E > 2)) ? 1 : 2)
+void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
   const int lane = (int)(gtid % LPC);
@@ -985,6 +946,10 @@ __global__ __launch_bounds__(256, (MASS == 2 || E > 2) ? 1 : 2) void nuts_kernel
       joint0 = lp - kin;
       const u32x4 kw = draw_block_s(a.seed, cid, st, TAG_NUTS_EXP, 0u);
       key = nuts_key(kw);
+      // (the table-driven Box-Muller of spec v5 for these momenta and this
+      // Exp1 draw measured -4 % at cfg3, profiles/r04/ab_nuts_tab_momenta.log:
+      // its 6 KiB of LDS tables and ~10 registers cost more than its
+      // instructions save)
       logu = joint0 + glog_pos(Unif<T>::oc(kw.z, kw.w));  // joint - Exp1
 #pragma unroll
       for (int e = 0; e < E; ++e) {

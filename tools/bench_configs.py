@@ -60,7 +60,7 @@ def cfg3(a):
     return {"config": "cfg3 NUTS DenseGaussian32 f64", "chains": C, "layout": "%dx%d" % s.layout(),
             "mass_adaptation": a.nuts_mass,
             "warmup_s": tw, "sample_s": ts, "leapfrogs": int(lf), "leapfrog_per_s": lf / ts,
-            "mean_tree_leapfrogs": lf / (C * a.nuts_collect), "plan": s.launch_plan(), "eps_median": float(np.median(eps)),
+            "mean_tree_leapfrogs": lf / (C * a.nuts_collect), "plan": s.launch_plan() if hasattr(s._lib, "gm_nuts_get_plan") else None, "eps_median": float(np.median(eps)),
             "ess_mean": float(ess.mean()), "ess_min": float(ess.min()), "rhat_max": float(rhat.max()),
             "ess_per_s": float(ess.mean()) / ts}
 

@@ -26,7 +26,7 @@ for step in "$@"; do
     diag) run diag_fullsize 600 python -u tools/diag_fullsize.py gpurun_out/diag_fullsize.jsonl ;;
     diagtest) run diag_tests 600 python -u -m pytest tests/test_gpu_diag_fullsize.py -x -v --timeout 300 --timeout-method thread ;;
     abmh) AB_ROUNDS=${AB_ROUNDS:-3} run ab_mh 600 python tools/ab_mh.py ${AB_LIBS} ;;
-    abnuts) AB_ROUNDS=${AB_ROUNDS:-3} run ab_nuts 900 python tools/ab_nuts.py ${AB_LIBS} ;;
+    abnuts) AB_ROUNDS=${AB_ROUNDS:-3} run ab_nuts 900 python tools/ab_nuts.py general-mcmc_amd/lib/libgmcmc.so ${AB_LIBS} ;;
     nlevels) run nuts_levels 300 python tools/probe_nuts_levels.py ;;
     nutstest) run nuts_tests 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_mfma_gauss.py tests/test_gpu_nuts_truncation.py tests/test_gpu_nuts_mass.py tests/test_gpu_fullsize_edge.py tests/test_gpu_checkpoint.py tests/test_gpu_step.py -x -q -k "nuts or NUTS or cfg3 or mfma" --timeout 120 --timeout-method thread ;;
     masstest) run mass_tests 300 python -u -m pytest tests/test_gpu_nuts_mass.py tests/test_gpu_mfma_gauss.py tests/test_gpu_nuts_truncation.py -x -q --timeout 120 --timeout-method thread ;;

@@ -104,6 +104,10 @@ def measure(prof_dir, kernel, grid, ordinal, simds=1024):
             "salu_insts_per_wave": sq["SQ_INSTS_SALU"] / waves if "SQ_INSTS_SALU" in sq else None,
             "wave_valu_active_frac": sq["SQ_ACTIVE_INST_VALU"] / max(sq["SQ_WAVE_CYCLES"], 1),
             "wave_wait_frac": sq["SQ_WAIT_ANY"] / max(sq["SQ_WAVE_CYCLES"], 1),
+            "wave_issue_stall_frac": (sq["SQ_WAIT_INST_ANY"] / max(sq["SQ_WAVE_CYCLES"], 1)
+                                      if "SQ_WAIT_INST_ANY" in sq else None),
+            "lds_insts_per_wave": sq["SQ_INSTS_LDS"] / waves if "SQ_INSTS_LDS" in sq else None,
+            "salu_per_valu": (sq["SQ_INSTS_SALU"] / max(sq["SQ_INSTS_VALU"], 1)) if "SQ_INSTS_SALU" in sq else None,
             "waves": waves, "clock_ghz": cycles / dur / 1e9,
             "note": "issue_frac = SQ_INSTS_VALU x 2 cycles (wave64 on a SIMD-32) / (1024 SIMDs x "
                     "GRBM_GUI_ACTIVE/8); per-wave counts are SQ_INSTS_* / SQ_WAVES",
