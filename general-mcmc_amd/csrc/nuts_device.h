@@ -792,7 +792,8 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   if (a.t0 == 0) record(0);
 
   long long acc = 0, nlf = 0;
-  NormalCache<T> ncache[E];
+  NormalCache<T> ncache[E];  // (one joint refill of the lane's E coordinates
+                             // measured -6 %, profiles/r04/ab_nuts_joint_momentum_refill.log)
   const bool track = a.trk.mean != nullptr;  // run_progress (generic_nuts.rs:688-704)
   ChainTrack<LPC, E> tr;
   if (track) tr.load(a.trk, c, lane, D);
