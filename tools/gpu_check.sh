@@ -32,6 +32,12 @@ for step in "$@"; do
     masstest) run mass_tests 300 python -u -m pytest tests/test_gpu_nuts_mass.py tests/test_gpu_mfma_gauss.py tests/test_gpu_nuts_truncation.py -x -q --timeout 120 --timeout-method thread ;;
     densemass) run dense_lds0 300 python tools/bench_configs.py --which 3 --nuts-mass dense --nuts-dense-forms 0,0 &&
                run dense_lds1 300 python tools/bench_configs.py --which 3 --nuts-mass dense --nuts-dense-forms 1,1  ;;
+    abbench) AB_ROUNDS=${AB_ROUNDS:-4} run ab_bench 600 python tools/ab_bench.py general-mcmc_amd/lib/libgmcmc.so ${AB_LIBS} ;;
+    denseforms)
+      for r in 1 2; do for f in 2,1 1,0 1,1; do
+        run dense_forms 300 python tools/bench_configs.py --which 3 --nuts-mass dense --nuts-dense-forms $f &&
+          sed "s|^{|{\"forms\": \"$f\", |" gpurun_out/dense_forms.log | grep '^{' >> gpurun_out/dense_forms.jsonl
+      done; done ;;
     mhtest) run mh_tests 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize_edge.py tests/test_gpu_tracker.py -x -q -k "mh or MH or cfg5 or Metropolis or tracker" --timeout 120 --timeout-method thread ;;
     warmup) run warmup_probe 300 python tools/probe_warmup.py ;;
     hostpath) run host_path 120 python tools/probe_host_path.py ;;
