@@ -338,8 +338,9 @@ template <class T, int E> struct RosenbrockLane {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const T tprev = (e > 0) ? t[(e > 0) ? e - 1 : 0] : tp;
-        // g = x (4b t - 2) + 2a - 2b t_prev as three fused multiply-adds
-        g[e] = gfma(nb2m[e], tprev, gfma(x[e], gfma(b4m[e], t[e], nc2m[e]), cam[e]));
+        // g = x (4b t - 2) + (2a - 2b t_prev) as three fused multiply-adds,
+        // the t_prev term beside the t chain (two dependent fmas after t)
+        g[e] = gfma(x[e], gfma(b4m[e], t[e], nc2m[e]), gfma(nb2m[e], tprev, cam[e]));
         if (LOGP) {
           const T am = a - x[e];
           const T s = keep(b * (t[e] * t[e]) + am * am, ms[e]);
@@ -381,7 +382,7 @@ template <class T, int E> struct RosenbrockLane {
       for (int e = 0; e < E; ++e) {
         const T xn = (e + 1 < E) ? x[(e + 1 < E) ? e + 1 : e] : nx;
         const T te = xn - x[e] * x[e];
-        g[e] = gfma(-b2, tprev, gfma(x[e], gfma(b4, te, (T)-2), (T)2 * a));
+        g[e] = gfma(x[e], gfma(b4, te, (T)-2), gfma(-b2, tprev, (T)2 * a));
         if (LOGP) {
           const T am = a - x[e];
           const T s = b * (te * te) + am * am;
@@ -400,7 +401,7 @@ template <class T, int E> struct RosenbrockLane {
         const bool hs = i <= Dv - 2, hp = (i >= 1) & (i <= Dv - 1);
         const T xn = (e + 1 < E) ? x[(e + 1 < E) ? e + 1 : e] : nx;
         const T te = xn - x[e] * x[e];
-        g[e] = gfma(hp ? -b2 : (T)0, tprev, gfma(x[e], gfma(hs ? b4 : (T)0, te, hs ? (T)-2 : (T)0), hs ? (T)2 * a : (T)0));
+        g[e] = gfma(x[e], gfma(hs ? b4 : (T)0, te, hs ? (T)-2 : (T)0), gfma(hp ? -b2 : (T)0, tprev, hs ? (T)2 * a : (T)0));
         if (LOGP) {
           const T am = a - x[e];
           const T s = hs ? b * (te * te) + am * am : (T)0;

@@ -36,6 +36,10 @@ hipError_t launch_hmc(gm_dtype dt, const TargetDev& tg, const Layout& lay, const
       return launch_timed(hmc_wide_kernel<T, E, TG>, dim3((unsigned)a.C), dim3(lay.lanes), 0, st, ev, a, t);
     });
   }
+  // (two chains per wave on packed f32 arithmetic, 13 VALU per two
+  // chain-leapfrogs instead of 22, bitwise equal, measured no faster: at the
+  // 2 waves per SIMD it leaves at 4096 chains the loop is latency-bound,
+  // profiles/r04/ab_hmc_packed_and_fma_order.log; not kept)
   return dispatch(dt, tg, lay, [&]<class T, int LPC, int E, class TG>(TG t) -> hipError_t {
     const size_t lds = t.template lds_bytes<LPC, E>();
     const long long threads = a.C * LPC;

@@ -77,6 +77,27 @@ def test_hmc_samples_bitwise(gm, oracle, dtype, dim, lay):
         s.close()
 
 
+@pytest.mark.parametrize("dim,elems", [(33, 1), (50, 1), (64, 1), (65, 2), (100, 2), (128, 2)])
+@pytest.mark.parametrize("n_chains,offset", [(2, 0), (10, 7), (11, 3), (64, 1)])
+def test_hmc_64lane_rosenbrock_bitwise(gm, oracle, dim, elems, n_chains, offset):
+    """RosenbrockND f32 at 64 x 1 and 64 x 2 (cfg2's and cfg4's layouts, the
+    64-lane gradient form): the oracle's bits for padded dims, even and odd
+    chain counts, odd global chain offsets and launches that start mid draw
+    block."""
+    x0 = start(gm, n_chains, dim, np.float32, 0.8)
+    t = gm.RosenbrockND()
+    s = gm.HMC(t, x0, 0.02, 9, dtype=np.float32, chain_offset=offset).set_seed(21)
+    s.set_layout(64, elems)
+    s.set_steps_per_launch(3)
+    out = s.run(5, 2)
+    q, samples, acc = oracle.hmc_run(Target.from_product(t, dim), x0, 0.02, 9, 21, 0, 7, 2, 64, elems,
+                                     chain_offset=offset)
+    np.testing.assert_array_equal(out, samples.transpose(1, 0, 2))
+    np.testing.assert_array_equal(s.positions(), q)
+    np.testing.assert_array_equal(s.accept_counts(), acc)
+    s.close()
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 def test_hmc_sharding_invariance(gm, dtype):
     """Chains keyed by global id: one sampler over 48 chains == two shards."""
