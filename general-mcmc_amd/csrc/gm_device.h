@@ -512,9 +512,9 @@ extern __shared__ __attribute__((aligned(16))) unsigned char gm_dyn_lds[];
 #ifndef GM_GEMV_UNROLL
 #define GM_GEMV_UNROLL 4  // columns of the LDS GEMV loop in flight per iteration
 #endif
-// matrix-core form: a chain's d / w slot in LDS, 32 doubles padded to 34 so
-// that the 4 chains of a wave fall in different banks (16-byte aligned)
-#define GM_MF_SLOT 34
+// matrix-core form: a chain's d slot in LDS, 16E doubles padded by 2 so that
+// the 4 chains of a wave fall in different banks (16-byte aligned)
+template <int E> __host__ __device__ constexpr int gm_mf_slot() { return 16 * E + 2; }
 template <class T, int LPC, int E> struct GaussLane;
 template <class T> struct GaussT {
   const T* mu;    // [D] device
@@ -522,13 +522,17 @@ template <class T> struct GaussT {
   T nc;
   int D;
   int use_lds = 0;
-  // the matrix-core form applies to layout (LPC, E) (at D <= 32)
+  // the matrix-core form applies to layout (LPC, E) (at D <= 16 E): f64, a
+  // chain on one 16-lane row with 2 (D <= 32) or 4 (D <= 64) coordinates per lane
   template <int LPC, int E> __host__ __device__ static constexpr bool mfma_form() {
-    return sizeof(T) == 8 && LPC == 16 && E == 2;
+    return sizeof(T) == 8 && LPC == 16 && (E == 2 || E == 4);
   }
+  // P's fragments: 4E K-steps x 64 lanes x E output groups (1024 doubles at E = 2)
+  template <int E> __host__ __device__ static constexpr int mf_frag() { return 64 * 4 * E * E; }
   // dynamic LDS bytes a 256-thread block needs for layout (LPC, E)
   template <int LPC, int E> __host__ __device__ static size_t lds_need(int D) {
-    if (mfma_form<LPC, E>() && D <= 32) return ((size_t)1024 + (size_t)(256 / LPC) * GM_MF_SLOT) * sizeof(T);
+    if (mfma_form<LPC, E>() && D <= 16 * E)
+      return ((size_t)mf_frag<E>() + (size_t)(256 / LPC) * gm_mf_slot<E>()) * sizeof(T);
     return ((size_t)D * LPC * E + (size_t)256 * E) * sizeof(T);
   }
   template <int LPC, int E> __host__ __device__ size_t lds_bytes() const {
@@ -546,16 +550,16 @@ template <class T> struct GaussT {
     r.sd = nullptr;
     r.mf = false;
     if constexpr (mfma_form<LPC, E>()) {
-      if (use_lds && D <= 32) {  // fragment order: k = (s * 64 + lane) * 2 + g
+      if (use_lds && D <= 16 * E) {  // fragment order: k = (s * 64 + lane) * E + g
         T* sp = (T*)gm_dyn_lds;
-        for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
-          const int l = (k >> 1) & 63, g = k & 1, st = k >> 7;
-          const int row = 8 * ((l >> 2) & 3) + 2 * (l & 3) + g, col = 4 * st + (l >> 4);
+        for (int k = threadIdx.x; k < mf_frag<E>(); k += blockDim.x) {
+          const int l = (k / E) & 63, g = k % E, st = k / (64 * E);
+          const int row = 4 * E * ((l >> 2) & 3) + E * (l & 3) + g, col = 4 * st + (l >> 4);
           sp[k] = (row < D && col < D) ? prec[(long long)col * D + row] : (T)0;
         }
         __syncthreads();
         r.sprec = sp;
-        r.sd = sp + 1024 + (threadIdx.x >> 4) * GM_MF_SLOT;
+        r.sd = sp + mf_frag<E>() + (threadIdx.x >> 4) * gm_mf_slot<E>();
         r.mf = true;
         return r;
       }
@@ -605,6 +609,8 @@ template <class T, int LPC, int E> struct GaussLane {
   __device__ __forceinline__ void mfma_product(const T (&d)[E], T (&w)[E]) const {
     if constexpr (GaussT<T>::template mfma_form<LPC, E>()) {
       typedef double v2 __attribute__((ext_vector_type(2)));
+      constexpr int KS = 4 * E;  // K-steps of 4 coordinates: D <= 16 E
+      constexpr int SL = gm_mf_slot<E>();
 #ifdef GM_NUTS_PROF
       const unsigned long long pt0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -616,28 +622,34 @@ template <class T, int LPC, int E> struct GaussLane {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int j = (l & 15) * E + e;
-        sd[(j & 3) * 8 + (j >> 2)] = d[e];
+        sd[(j & 3) * KS + (j >> 2)] = d[e];
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // A: chain l&3's d_{4s + (l>>4)}, s = 0..7
-      const T* at = sprec + 1024 + (wb + (l & 3)) * GM_MF_SLOT + (l >> 4) * 8;
-      v2 dv[4], pv[8];
+      // A: chain l&3's d_{4s + (l>>4)}, s = 0..KS-1
+      const T* at = sprec + GaussT<T>::template mf_frag<E>() + (wb + (l & 3)) * SL + (l >> 4) * KS;
+      v2 dv[KS / 2];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) dv[t] = *(const v2*)(at + 2 * t);
+      for (int t = 0; t < KS / 2; ++t) dv[t] = *(const v2*)(at + 2 * t);
+      // D[m = l>>4][n = l&3] of block (l>>2)&3: chain l>>4's w at E(l&15) + g, this lane's w[g];
+      // the E accumulations are independent chains, each in ascending s from +0
+      double acc[E];
 #pragma unroll
-      for (int t = 0; t < 8; ++t) pv[t] = *(const v2*)(sprec + (t * 64 + l) * 2);
-      // D[m = l>>4][n = l&3] of block (l>>2)&3: chain l>>4's w at 2(l&15) + g, this lane's w[g]
-      double acc0 = 0.0, acc1 = 0.0;
+      for (int g = 0; g < E; ++g) acc[g] = 0.0;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
+      for (int s = 0; s < KS; ++s) {
         const double a = dv[s >> 1][s & 1];
-        acc0 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, pv[s][0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, pv[s][1], acc1, 0, 0, 0);
+        const T* pb = sprec + (s * 64 + l) * E;
+#pragma unroll
+        for (int g = 0; g < E; g += 2) {
+          const v2 pv = *(const v2*)(pb + g);
+          acc[g] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, pv[0], acc[g], 0, 0, 0);
+          acc[g + 1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, pv[1], acc[g + 1], 0, 0, 0);
+        }
       }
-      w[0] = acc0;
-      w[1] = acc1;
+#pragma unroll
+      for (int g = 0; g < E; ++g) w[g] = acc[g];
 #ifdef GM_NUTS_PROF
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the product's last read has landed
       prof_prod += __builtin_amdgcn_s_memtime() - pt0;

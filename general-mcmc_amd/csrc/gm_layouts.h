@@ -52,8 +52,10 @@ hipError_t dispatch_target(const TargetDev& tg, F& f) {
       t.prec = (const T*)tg.prec;
       t.nc = (T)tg.norm_const;
       t.D = tg.D;
-      // LDS staging while it leaves room for >= 4 blocks (16 waves) per CU
-      t.use_lds = GaussT<T>::template lds_need<LPC, E>(tg.D) <= 40 * 1024;
+      // LDS staging while it leaves room for >= 4 blocks (16 waves) per CU,
+      // or for the matrix-core form (f64 16 x 4 at D <= 64: 41 KiB)
+      t.use_lds = GaussT<T>::template lds_need<LPC, E>(tg.D) <= 40 * 1024 ||
+                  (GaussT<T>::template mfma_form<LPC, E>() && tg.D <= 16 * E);
       return f.template operator()<T, LPC, E>(t);
     }
     default:
