@@ -463,6 +463,48 @@ __device__ __forceinline__ bool no_uturn_m(const MassDev<T, E, K>& M, const T (&
   return dm >= (T)0 && dp >= (T)0;
 }
 
+// The same two criteria from the trajectory's ends without ordering them: x
+// the end on side v (being integrated) and o the other one. The minus-to-plus
+// difference is q+ - q- = v (x_q - o_q), exactly (IEEE subtraction is
+// antisymmetric up to the sign of a zero), so each per-lane product and every
+// stage of the group sum is the negation of the ordered form's when v < 0:
+// the sums differ at most in the sign of a zero, which `>= 0` does not see,
+// and NaN fails either way. The two tests ((q+ - q-).p- and .p+) are the
+// pair {S_o, S_x} in some order, and both must hold. So the decision is the
+// ordered form's bit for bit, without the 4E selects that ordered the ends.
+template <int LPC, int E, class T>
+__device__ __forceinline__ bool no_uturn_ends(const T (&xq)[E], const T (&oq)[E], const T (&xp)[E],
+                                              const T (&op)[E], int v) {
+  T d[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) d[e] = xq[e] - oq[e];
+  T dd[2];
+  dd[0] = d[0] * op[0];
+  dd[1] = d[0] * xp[0];
+#pragma unroll
+  for (int e = 1; e < E; ++e) {
+    dd[0] = dd[0] + d[e] * op[e];
+    dd[1] = dd[1] + d[e] * xp[e];
+  }
+  group_sum_n<LPC>(dd);
+  const T sv = (T)v;
+  return sv * dd[0] >= (T)0 && sv * dd[1] >= (T)0;
+}
+template <int LPC, int E, class T, int K>
+__device__ __forceinline__ bool no_uturn_ends_m(const MassDev<T, E, K>& M, const T (&xq)[E], const T (&oq)[E],
+                                                const T (&xp)[E], const T (&op)[E], int v, int lane) {
+  if (M.kind() == 0) return no_uturn_ends<LPC, E>(xq, oq, xp, op, v);
+  T d[E], vo[E], vx[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) d[e] = xq[e] - oq[e];
+  inv_mul<LPC, E>(M, op, vo, lane);
+  inv_mul<LPC, E>(M, xp, vx, lane);
+  const T so = dot_group<LPC, E>(d, vo);
+  const T sx = dot_group<LPC, E>(d, vx);
+  const T sv = (T)v;
+  return sv * so >= (T)0 && sv * sx >= (T)0;
+}
+
 template <int LPC, class T>
 __device__ __forceinline__ bool all_finite(const T (&x)[1]) { return true; }
 
@@ -884,14 +926,14 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
 #ifdef GM_NUTS_PROF
     GM_PSEG(0);
 #endif
-    if constexpr (MASS == 0) {  // leapfrog (:1396-1418), as selects: kick, drift
-      const bool adv = live && !starting;
+    if constexpr (MASS == 0) {  // leapfrog (:1396-1418): kick, drift
+      // unconditionally: a starting chain overwrites its edge with the
+      // transition's start below, and a finished chain's edge is never read
+      // again, so neither needs the old values kept (no selects)
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const T pk = pe[e] + ge[e] * h;
-        const T qk = qe[e] + pk * epsv;
-        pe[e] = adv ? pk : pe[e];
-        qe[e] = adv ? qk : qe[e];
+        pe[e] = pe[e] + ge[e] * h;
+        qe[e] = qe[e] + pe[e] * epsv;
       }
     } else if (live && !starting) {  // leapfrog_with_mass (:1396-1418): kick, drift by M^-1 p
 #pragma unroll
@@ -911,14 +953,8 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
 #ifdef GM_NUTS_PROF
     GM_PSEG(2);
 #endif
-    {
-      const bool adv = live && !starting;
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const T pk = pe[e] + gx[e] * h;
-        pe[e] = adv ? pk : pe[e];
-      }
-    }
+    for (int e = 0; e < E; ++e) pe[e] = pe[e] + gx[e] * h;  // (unconditionally, as above)
     {
       T pk[E];
 #pragma unroll
@@ -1016,15 +1052,9 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       }
       tn = ln_ + tn;
       {
-        T qm[E], qp[E], pm[E], pp[E];  // U-turn over the merged subtree's ends, minus side first
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          qm[e] = v > 0 ? lq[e] : qe[e];
-          qp[e] = v > 0 ? qe[e] : lq[e];
-          pm[e] = v > 0 ? lpv[e] : pe[e];
-          pp[e] = v > 0 ? pe[e] : lpv[e];
-        }
-        const bool nu = no_uturn<LPC, E>(qm, qp, pm, pp);
+        // U-turn over the merged subtree's ends: the edge (qe, pe) and the
+        // left sibling's first point (lq, lpv), unordered (no_uturn_ends)
+        const bool nu = no_uturn_ends<LPC, E>(qe, lq, pe, lpv, v);
         ts = ts && nu;
       }
       ta = lal + ta;
@@ -1058,18 +1088,12 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       n += tn;
       bool s_ok = ts;
       {
-        T qmv[E], qpv[E], pmv[E], ppv[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          qmv[e] = v > 0 ? qf[e] : qe[e];
-          qpv[e] = v > 0 ? qe[e] : qf[e];
-          pmv[e] = v > 0 ? pf[e] : pe[e];
-          ppv[e] = v > 0 ? pe[e] : pf[e];
-        }
+        // the trajectory's ends: the edge (qe, pe) on side v and the far end
+        // (qf, pf), unordered (no_uturn_ends)
         if constexpr (MASS == 2) {  // the dense products: only where needed
-          if (s_ok) s_ok = no_uturn_m<LPC, E>(M, qmv, qpv, pmv, ppv, lane);
+          if (s_ok) s_ok = no_uturn_ends_m<LPC, E>(M, qe, qf, pe, pf, v, lane);
         } else {
-          const bool nu = no_uturn_m<LPC, E>(M, qmv, qpv, pmv, ppv, lane);
+          const bool nu = no_uturn_ends_m<LPC, E>(M, qe, qf, pe, pf, v, lane);
           s_ok = s_ok && nu;
         }
       }
