@@ -658,6 +658,9 @@ template <class T, int LPC, int E> struct GaussLane {
   }
   template <int LPC_, int E_, bool LOGP>
   __device__ __forceinline__ T eval_impl(const T (&x)[E], T (&g)[E], int lane) const {
+    // (a mask-free copy for chains that fill their lanes, chosen by a
+    // wave-uniform branch, measured -15 % at cfg3: the duplicated evaluation,
+    // profiles/r04/ab_nuts_maskfree_gauss_eval.log; not kept)
     static_assert(LPC_ == LPC && E_ == E, "layout mismatch");
     T d[E], w[E];
 #pragma unroll
