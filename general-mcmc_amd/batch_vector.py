@@ -10,8 +10,12 @@ reference's step order (batched_hmc.rs:129-190).
 
 The fused sampler (`HMC`) is the performance path. This op-by-op path is
 for callers that plug their own step logic into the seam. A step composed here
-equals the fused kernel's step bit for bit: the random fills read the same
-Philox streams, and the reductions use the same order.
+reads the same Philox streams and reduces in the same order as the fused
+kernel; its kicks and drift are the reference's `add_scaled_assign` (product
+and sum rounded separately, euclidean.rs:392-394), where the fused kernel uses
+fused multiply-adds, so the two agree to rounding and each matches its own
+form of the oracle bit for bit. With `fused_leapfrog=True` the leapfrog is
+one `gm_bv_leapfrog` kernel in the fused kernel's form (its bits).
 """
 from __future__ import annotations
 
@@ -241,7 +245,8 @@ class BatchedGenericHMC:
         self.seed = int(seed)
         self.chain_offset = int(chain_offset)
         self.t = 0  # transition index (keys the random streams)
-        # one gm_bv_leapfrog kernel per leapfrog instead of four ops (same bits)
+        # one gm_bv_leapfrog kernel per leapfrog instead of four ops (the fused
+        # kernel's fused multiply-add kicks and drift: its bits)
         self.fused_leapfrog = bool(fused_leapfrog)
 
     def set_seed(self, seed: int) -> "BatchedGenericHMC":

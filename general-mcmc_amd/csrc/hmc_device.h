@@ -125,25 +125,23 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
       g1[e] = g[e];
     }
     // 5. leapfrog: L-1 gradient-only steps, then the last one with logp.
-    // gh = g*(0.5 eps) is shared by the closing kick of one step and the
-    // opening kick of the next (same operands, same bits).
+    // The kicks p + g*(eps/2) and the drift q + p*eps are the engine's fused
+    // multiply-adds (one rounding each; the reference's tensor ops round the
+    // product and the sum separately, batched_hmc.rs:166-190): 9 VALU per
+    // 64-lane Rosenbrock leapfrog instead of 11 (+9 % headline,
+    // profiles/r04/ab_hmc_fma_kick_drift.log); the oracle's engine form is
+    // the same (gm_oracle_t.inc hmc_chains, form 0).
     T lp1 = lp;
-    T gh[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) gh[e] = g1[e] * half;
     // (unrolled by hand: the DPP intrinsics are convergent, so the compiler
     // will not runtime-unroll, and a taken branch costs a wave ~20 cycles)
     auto lf = [&]() __attribute__((always_inline)) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) p1[e] = p1[e] + gh[e];
+      for (int e = 0; e < E; ++e) p1[e] = gfma(g1[e], half, p1[e]);
 #pragma unroll
-      for (int e = 0; e < E; ++e) q1[e] = q1[e] + p1[e] * eps;
+      for (int e = 0; e < E; ++e) q1[e] = gfma(p1[e], eps, q1[e]);
       tg.template eval<LPC, E, false>(q1, g1, lane);
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        gh[e] = g1[e] * half;
-        p1[e] = p1[e] + gh[e];
-      }
+      for (int e = 0; e < E; ++e) p1[e] = gfma(g1[e], half, p1[e]);
     };
     int l = 0;
     if (a.lf_unroll == 4)
@@ -162,9 +160,9 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
     T ke1;
     if (a.L >= 1) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) p1[e] = p1[e] + gh[e];
+      for (int e = 0; e < E; ++e) p1[e] = gfma(g1[e], half, p1[e]);
 #pragma unroll
-      for (int e = 0; e < E; ++e) q1[e] = q1[e] + p1[e] * eps;
+      for (int e = 0; e < E; ++e) q1[e] = gfma(p1[e], eps, q1[e]);
       using TL = typename Bare<decltype(tg)>::type;  // the per-lane target view
       if constexpr (requires { TL::template has_part<LPC>; }) {
         if constexpr (TL::template has_part<LPC>) {
@@ -172,7 +170,7 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
           T sums[2];
           sums[0] = tg.template eval_part<LPC, E>(q1, g1, lane);
 #pragma unroll
-          for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+          for (int e = 0; e < E; ++e) p1[e] = gfma(g1[e], half, p1[e]);
           sums[1] = kin_part();
           group_sum_n<LPC>(sums);
           lp1 = tg.finish(sums[0]);
@@ -180,13 +178,13 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
         } else {
           lp1 = tg.template eval<LPC, E, true>(q1, g1, lane);
 #pragma unroll
-          for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+          for (int e = 0; e < E; ++e) p1[e] = gfma(g1[e], half, p1[e]);
           ke1 = group_sum<LPC>(kin_part()) * (T)0.5;
         }
       } else {
         lp1 = tg.template eval<LPC, E, true>(q1, g1, lane);
 #pragma unroll
-        for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+        for (int e = 0; e < E; ++e) p1[e] = gfma(g1[e], half, p1[e]);
         ke1 = group_sum<LPC>(kin_part()) * (T)0.5;
       }
     } else {
@@ -293,13 +291,13 @@ __global__ __launch_bounds__(gm_wide_max_threads(sizeof(T), E)) void hmc_wide_ke
     T lp1 = lp;
     for (int l = 0; l < a.L; ++l) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+      for (int e = 0; e < E; ++e) p1[e] = gfma(g1[e], half, p1[e]);
 #pragma unroll
-      for (int e = 0; e < E; ++e) q1[e] = q1[e] + p1[e] * eps;
+      for (int e = 0; e < E; ++e) q1[e] = gfma(p1[e], eps, q1[e]);
       if (l + 1 < a.L) tg.template eval_wide<E, false>(q1, g1, cx);
       else lp1 = tg.template eval_wide<E, true>(q1, g1, cx);
 #pragma unroll
-      for (int e = 0; e < E; ++e) p1[e] = p1[e] + g1[e] * half;
+      for (int e = 0; e < E; ++e) p1[e] = gfma(g1[e], half, p1[e]);
     }
     // 6. proposed kinetic energy
     T kq = (T)0;

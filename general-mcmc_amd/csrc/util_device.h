@@ -34,9 +34,10 @@ __global__ __launch_bounds__(256) void logp_grad_kernel(long long n, int D, cons
 
 // One leapfrog of every chain with the state in HBM (the reference's
 // BatchedGenericHMC::leapfrog loop body, batched_hmc.rs:166-190, as one
-// kernel): p += g*(eps/2); q += p*eps; (logp, g) = target(q); p += g*(eps/2).
-// The same operations as the fused hmc_kernel and as the composed tier-2 ops
-// (add_scaled_assign x2, logp_and_grad, add_scaled_assign), so the same bits.
+// kernel): p += g*(eps/2); q += p*eps; (logp, g) = target(q); p += g*(eps/2),
+// the kicks and the drift as the fused hmc_kernel's fused multiply-adds, so
+// the same bits as that kernel (the composed tier-2 ops round the product and
+// the sum separately, as the reference's add_scaled_assign).
 // Per chain-leapfrog it moves exactly SURVEY.md's B_alg = (6D+1)*sizeof(T)
 // bytes: the per-leapfrog design the HBM roofline is defined for.
 template <class T, int LPC, int E, class TG>
@@ -58,12 +59,12 @@ __global__ __launch_bounds__(256) void leapfrog_hbm_kernel(long long n, int D, T
     g[e] = (i < D) ? gs[c * D + i] : (T)0;
   }
 #pragma unroll
-  for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * half;
+  for (int e = 0; e < E; ++e) p[e] = gfma(g[e], half, p[e]);
 #pragma unroll
-  for (int e = 0; e < E; ++e) q[e] = q[e] + p[e] * eps;
+  for (int e = 0; e < E; ++e) q[e] = gfma(p[e], eps, q[e]);
   const T lp = tg.template eval<LPC, E, true>(q, g, lane);
 #pragma unroll
-  for (int e = 0; e < E; ++e) p[e] = p[e] + g[e] * half;
+  for (int e = 0; e < E; ++e) p[e] = gfma(g[e], half, p[e]);
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     const int i = lane * E + e;

@@ -68,13 +68,15 @@ float or_nuts_u_f(uint64_t key, uint32_t idx);
 double or_logp_grad_d(const or_target* t, int lanes, int elems, const double* x, double* g);
 float or_logp_grad_f(const or_target* t, int lanes, int elems, const float* x, float* g);
 
-/* ---- HMC: batched_hmc.rs:129-190 per chain ---- */
+/* ---- HMC: batched_hmc.rs:129-190 per chain; form 0 the engine's fused
+ * multiply-add kicks and drift (the kernels), 1 the reference's op structure
+ * (two roundings each: the composed tier-2 ops) ---- */
 int or_hmc_run_d(const or_target* t, int lanes, int elems, int64_t C, int D, double* q, double eps,
                  int L, uint64_t seed, uint64_t step0, uint32_t chain_offset, int64_t n_steps,
-                 int64_t collect_from, double* samples, int64_t* accepts, int threads);
+                 int64_t collect_from, double* samples, int64_t* accepts, int threads, int form);
 int or_hmc_run_f(const or_target* t, int lanes, int elems, int64_t C, int D, float* q, double eps,
                  int L, uint64_t seed, uint64_t step0, uint32_t chain_offset, int64_t n_steps,
-                 int64_t collect_from, float* samples, int64_t* accepts, int threads);
+                 int64_t collect_from, float* samples, int64_t* accepts, int threads, int form);
 
 /* ---- MH: metropolis_hastings.rs:306-318 per chain ---- */
 int or_mh_run_d(const or_target* t, int lanes, int elems, int64_t C, int D, double* q,

@@ -58,7 +58,7 @@ def load():
         getattr(lib, f"or_logp_grad_{sfx}").restype = rt
         getattr(lib, f"or_logp_grad_{sfx}").argtypes = [tp, _int, _int, _vp, _vp]
         getattr(lib, f"or_hmc_run_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _dbl, _int,
-                                                      _u64, _u64, _u32, _i64, _i64, _vp, _vp, _int]
+                                                      _u64, _u64, _u32, _i64, _i64, _vp, _vp, _int, _int]
         getattr(lib, f"or_mh_run_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _dbl, _u64,
                                                      _u64, _u32, _i64, _i64, _vp, _vp, _int]
         getattr(lib, f"or_nuts_run_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _vp, _vp,
@@ -210,7 +210,10 @@ class Oracle:
         return lp, np.ascontiguousarray(g[:, :d])
 
     def hmc_run(self, target: Target, q, eps, L, seed, step0, n_steps, collect_from, lanes, elems,
-                chain_offset=0, threads=8):
+                chain_offset=0, threads=8, form=0):
+        """form 0: the engine's leapfrog (fused multiply-add kicks and drift,
+        the kernels); 1: the reference's op structure (the composed tier-2
+        ops)."""
         q = np.array(q, copy=True, order="C")
         C_, D = q.shape
         rows = max(0, n_steps - collect_from)
@@ -219,7 +222,7 @@ class Oracle:
         t = target.struct()
         rc = getattr(self.lib, f"or_hmc_run_{_sfx(q.dtype)}")(
             C.byref(t), lanes, elems, C_, D, _p(q), eps, L, seed, step0, chain_offset, n_steps,
-            collect_from, _p(samples), _p(acc), threads)
+            collect_from, _p(samples), _p(acc), threads, form)
         assert rc == 0
         return q, samples, acc
 
