@@ -91,14 +91,22 @@ __global__ __launch_bounds__(1024) void bv_dot_kernel(long long n, const T* __re
   if (threadIdx.x == 0) out[0] = (double)part[0];
 }
 
-// fill_random_normal (euclidean.rs:484-496): N(0,1) from the momentum stream
+// fill_random_normal (euclidean.rs:484-496): N(0,1) from the momentum stream,
+// the HMC kernels' momentum draws (gm_rng.h momenta_of: the f32 table form)
 template <class T>
 __global__ void bv_normal_kernel(long long C, int D, T* __restrict__ out, uint64_t seed,
                                  uint32_t chain_offset, uint64_t step, uint32_t tag) {
+  __shared__ BmLds32 bm32[1];
+  if constexpr (sizeof(T) == 4) {
+    bm_lds_fill32(bm32[0]);
+    __syncthreads();
+  }
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= C * D) return;
   const uint32_t c = (uint32_t)(k / D), i = (uint32_t)(k % D);
-  out[k] = normal<T>(seed, chain_offset + c, step, tag, i);
+  T z[Blk<T>::S];
+  momenta_of(draw_block(seed, chain_offset + c, step / Blk<T>::S, tag, i), z, bm32[0]);
+  out[k] = pick(z, (int)(step % Blk<T>::S));
 }
 
 // sample_uniform (euclidean.rs:498-509): one [0,1) uniform per chain

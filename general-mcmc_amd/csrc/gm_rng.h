@@ -22,6 +22,9 @@
 // with z_{2j} = r cos(2 pi u_{2j+1}), z_{2j+1} = r sin(2 pi u_{2j+1}),
 // r = sqrt(-2 ln u_{2j}) (u_{2j} from the (0,1] form); the draw for `step` is
 // z_{step % S}. A kernel that runs consecutive steps computes each block once.
+// Spec v5 keeps these pairs but evaluates ln and sin/cos from tables, with
+// explicit fused multiply-adds (normals_tab: the f64 MH proposals;
+// normals_tab32: the f32 HMC momenta); the oracle evaluates the same.
 //
 // Bit-exactness rules (both sides): only IEEE +,-,*,/ and sqrt (correctly
 // rounded on gfx950 and x86), no FMA contraction (-ffp-contract=off), and our
@@ -569,6 +572,61 @@ __device__ __forceinline__ void normals_tab(u32x4 x, double (&z)[2], const BmLds
   z[0] = rad * cv;
   z[1] = rad * sv;
 }
+
+// The f32 form (spec v5 for the f32 HMC momenta): the 4 normals of a block,
+// pairs (x.x, x.y) and (x.z, x.w) as normals_of(float), with f32 tables
+// (1/c_j rounded to f32 and ln of its reciprocal, sin/cos rounded):
+//   ln u1 = e ln2 + ln c_j + ln(1 + r), r = fma(m, 1/c_j, -1), |r| < 2^-8,
+//     ln(1 + r) to degree 3 (the next term < 2^-34);
+//   sin th to degree 3 and cos th - 1 to degree 4, th < 2 pi/256.
+// No division and no branch: 2 LDS reads and ~25 VALU per pair instead of
+// msun's logf (a division) and sinf/cosf polynomials.
+static __constant__ float gm_bm32_log[256] = {GM_BM32_LOG_INIT};
+static __constant__ float gm_bm32_sincos[512] = {GM_BM32_SINCOS_INIT};
+typedef float gm_bm_f2 __attribute__((ext_vector_type(2)));
+struct BmLds32 {  // the f32 tables as 8-byte pairs in LDS (3 KiB)
+  gm_bm_f2 lg[128], sc[256];
+};
+__device__ __forceinline__ void bm_lds_fill32(BmLds32& t) {
+  for (int k = threadIdx.x; k < 256; k += blockDim.x) {
+    if (k < 128) t.lg[k] = gm_bm_f2{gm_bm32_log[2 * k], gm_bm32_log[2 * k + 1]};
+    t.sc[k] = gm_bm_f2{gm_bm32_sincos[2 * k], gm_bm32_sincos[2 * k + 1]};
+  }
+}
+__device__ __forceinline__ void normal_pair_tab32(uint32_t w1, uint32_t w2, float& z0, float& z1,
+                                                  const BmLds32& t) {
+  const float u1 = Unif<float>::oc(w1, 0);
+  const uint32_t b = f2u(u1);
+  const int e = (int)(b >> 23) - 127;
+  const uint32_t mb = b & 0x007fffffu;
+  const float m = u2f(mb | 0x3f800000u);
+  const gm_bm_f2 lc = t.lg[mb >> 16];
+  const float r = __builtin_fmaf(m, lc.x, -1.0f);
+  const float l1 = __builtin_fmaf(r * r, __builtin_fmaf(r, 0x1.555556p-2f, -0.5f), r);
+  const float de = (float)e;
+  // e ln2 as msun's logf split (ln2_hi has 17 significant bits: de * ln2_hi is exact)
+  const float lnu = __builtin_fmaf(de, 6.9313812256e-01f, __builtin_fmaf(de, 9.0580006145e-06f, lc.y + l1));
+  const float m2l = -2.0f * lnu;
+  const float rad = gsqrt(m2l > 0.0f ? m2l : 0.0f);
+  const float u2 = Unif<float>::co(w2, 0);
+  const int j = (int)(u2 * 256.0f);
+  const float th = (u2 - (float)j * 0.00390625f) * 0x1.921fb6p+2f;
+  const float zz = th * th;
+  const float sth = __builtin_fmaf(th * zz, -0x1.555556p-3f, th);
+  const float cm = zz * __builtin_fmaf(zz, 0x1.555556p-5f, -0.5f);
+  const gm_bm_f2 sc = t.sc[j];
+  const float sv = __builtin_fmaf(sc.y, sth, __builtin_fmaf(sc.x, cm, sc.x));
+  const float cv = __builtin_fmaf(-sc.x, sth, __builtin_fmaf(sc.y, cm, sc.y));
+  z0 = rad * cv;
+  z1 = rad * sv;
+}
+__device__ __forceinline__ void normals_tab32(u32x4 x, float (&z)[4], const BmLds32& t) {
+  normal_pair_tab32(x.x, x.y, z[0], z[1], t);
+  normal_pair_tab32(x.z, x.w, z[2], z[3], t);
+}
+// the HMC momenta of a block: the f32 table form, msun's f64 pairs
+__device__ __forceinline__ void momenta_of(u32x4 x, float (&z)[4], const BmLds32& t) { normals_tab32(x, z, t); }
+__device__ __forceinline__ void momenta_of(u32x4 x, double (&z)[2], const BmLds32&) { normals_of(x, z); }
 #endif
 
 // A per-lane cache of one block of draws for consecutive steps.

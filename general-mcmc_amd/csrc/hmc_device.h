@@ -13,6 +13,13 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
   const long long c = gtid / LPC;
   const int lane = (int)(gtid % LPC);
   const auto tg = tg_.template bind<LPC, E>(lane);  // per-lane target view
+  // f32 momenta: the table-driven Box-Muller (gm_rng.h normals_tab32); its
+  // tables in LDS, filled by the whole block before any thread returns
+  __shared__ BmLds32 bm32[1];
+  if constexpr (sizeof(T) == 4) {
+    bm_lds_fill32(bm32[0]);
+    __syncthreads();
+  }
   if (c >= a.C) return;  // whole lane groups leave together
   const int D = a.D;
   T* __restrict__ qs = (T*)a.q;
@@ -47,7 +54,7 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
-      normals_of(draw_block(pk, cid, blk, TAG_MOM, (uint32_t)i), zs[e]);
+      momenta_of(draw_block(pk, cid, blk, TAG_MOM, (uint32_t)i), zs[e], bm32[0]);
 #pragma unroll
       for (int k = 0; k < S; ++k) zs[e][k] = (i < D) ? zs[e][k] : (T)0;
     }
@@ -235,6 +242,11 @@ __global__ __launch_bounds__(gm_wide_max_threads(sizeof(T), E)) void hmc_wide_ke
   const int tid = threadIdx.x;
   const long long c = blockIdx.x;
   const auto tg = tg_.template bind<64, E>(tid);  // coordinates tid*E + e
+  __shared__ BmLds32 bm32[1];  // f32 momenta: the table-driven Box-Muller
+  if constexpr (sizeof(T) == 4) {
+    bm_lds_fill32(bm32[0]);
+    __syncthreads();
+  }
   WideCtx<T> cx{tid >> 6, (int)(blockDim.x >> 6), tid & 63, xf, xl, red, 0};
   const int D = a.D;
   const long long Dp = (long long)blockDim.x * E;
@@ -266,7 +278,7 @@ __global__ __launch_bounds__(gm_wide_max_threads(sizeof(T), E)) void hmc_wide_ke
       for (int e = 0; e < E; ++e) {
         const int i = tid * E + e;
         T z[S];
-        normals_of(draw_block(a.seed, cid, st / S, TAG_MOM, (uint32_t)i), z);
+        momenta_of(draw_block(a.seed, cid, st / S, TAG_MOM, (uint32_t)i), z, bm32[0]);
 #pragma unroll
         for (int k = 0; k < S; ++k) zs[k * Dp + i] = (i < D) ? z[k] : (T)0;
       }

@@ -277,6 +277,53 @@ double or_tab_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t ta
   or_tab_normal_pair(x, z);
   return z[step % 2];
 }
+/* Spec v5 for the f32 HMC momenta (gm_rng.h normal_pair_tab32): the pair of
+ * words (w1, w2) as or_normal_f's Box-Muller pair, ln and sin/cos from the f32
+ * tables (1/c_j rounded to f32 and ln of its reciprocal; sin/cos rounded):
+ * ln(1 + r) to degree 3, sin th to degree 3, cos th - 1 to degree 4. */
+static const float bm32_log[256] = {GM_BM32_LOG_INIT};
+static const float bm32_sincos[512] = {GM_BM32_SINCOS_INIT};
+void or_tab_normal_pair_f(uint32_t w1, uint32_t w2, float z[2]) {
+  const float u1 = unif_oc_f(w1);
+  uint32_t b;
+  memcpy(&b, &u1, 4);
+  const int e = (int)(b >> 23) - 127;
+  const uint32_t mb = b & 0x007fffffu, mbits = mb | 0x3f800000u;
+  float m;
+  memcpy(&m, &mbits, 4);
+  const int jl = (int)(mb >> 16);
+  const float invc = bm32_log[2 * jl], logc = bm32_log[2 * jl + 1];
+  const float r = fmaf(m, invc, -1.0f);
+  const float l1 = fmaf(r * r, fmaf(r, 0x1.555556p-2f, -0.5f), r);
+  const float de = (float)e;
+  const float lnu = fmaf(de, 6.9313812256e-01f, fmaf(de, 9.0580006145e-06f, logc + l1));
+  const float m2l = -2.0f * lnu;
+  const float rad = sqrtf(m2l > 0.0f ? m2l : 0.0f);
+  const float u2 = unif_co_f(w2);
+  const int j = (int)(u2 * 256.0f);
+  const float th = (u2 - (float)j * 0.00390625f) * 0x1.921fb6p+2f;
+  const float zz = th * th;
+  const float sth = fmaf(th * zz, -0x1.555556p-3f, th);
+  const float cm = zz * fmaf(zz, 0x1.555556p-5f, -0.5f);
+  const float S = bm32_sincos[2 * j], Cc = bm32_sincos[2 * j + 1];
+  const float sv = fmaf(Cc, sth, fmaf(S, cm, S));
+  const float cv = fmaf(-S, sth, fmaf(Cc, cm, Cc));
+  z[0] = rad * cv;
+  z[1] = rad * sv;
+}
+/* the HMC momentum draw for `step` (TAG_MOM streams): f32 the table pairs of
+ * the block's 4 words, f64 msun's pair (spec v2) */
+float or_mom_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  uint32_t x[4];
+  float z[2];
+  block(seed, chain, step / 4, tag, idx, x);
+  const int k = (int)(step % 4), pair = k / 2;
+  or_tab_normal_pair_f(x[2 * pair], x[2 * pair + 1], z);
+  return z[k % 2];
+}
+double or_mom_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
+  return or_normal_d(seed, chain, step, tag, idx);
+}
 float or_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
 static float or_mh_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx) {
   return or_normal_f(seed, chain, step, tag, idx);
@@ -386,6 +433,7 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #define SQRT sqrt
 #define FMA fma
 #define NORMAL or_normal_d
+#define MOM_NORMAL or_mom_normal_d
 #define MH_NORMAL or_tab_normal_d
 #define UNIF_CO or_uniform_co_d
 #define UNIF_OC uniform_oc_d
@@ -400,6 +448,7 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #undef SQRT
 #undef FMA
 #undef NORMAL
+#undef MOM_NORMAL
 #undef MH_NORMAL
 #undef UNIF_CO
 #undef UNIF_OC
@@ -414,6 +463,7 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #define SQRT sqrtf
 #define FMA fmaf
 #define NORMAL or_normal_f
+#define MOM_NORMAL or_mom_normal_f
 #define MH_NORMAL or_mh_normal_f
 #define UNIF_CO or_uniform_co_f
 #define UNIF_OC uniform_oc_f

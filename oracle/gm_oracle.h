@@ -51,6 +51,11 @@ float or_exp_f(float x);
 double or_cos2pi_d(double u);
 float or_cos2pi_f(float u);
 double or_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
+/* spec v5 f32 (the HMC momenta): one table-driven Box-Muller pair of the
+ * words (w1, w2); the HMC momentum draws (f32 table form, f64 = or_normal_d) */
+void or_tab_normal_pair_f(uint32_t w1, uint32_t w2, float z[2]);
+float or_mom_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
+double or_mom_normal_d(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
 float or_normal_f(uint64_t seed, uint32_t chain, uint64_t step, uint32_t tag, uint32_t idx);
 /* the f64 MH proposal normal (spec v5: table-driven Box-Muller) */
 void or_tab_normal_pair(const uint32_t x[4], double z[2]);

@@ -48,11 +48,16 @@ def load():
         getattr(lib, f"or_cos2pi_{sfx}").argtypes = [rt]
         getattr(lib, f"or_normal_{sfx}").restype = rt
         getattr(lib, f"or_normal_{sfx}").argtypes = [_u64, _u32, _u64, _u32, _u32]
+        getattr(lib, f"or_mom_normal_{sfx}").restype = rt
+        getattr(lib, f"or_mom_normal_{sfx}").argtypes = [_u64, _u32, _u64, _u32, _u32]
         if sfx == "d":
             lib.or_tab_normal_d.restype = rt
             lib.or_tab_normal_d.argtypes = [_u64, _u32, _u64, _u32, _u32]
             lib.or_tab_normal_pair.restype = None
             lib.or_tab_normal_pair.argtypes = [_vp, _vp]
+        else:
+            lib.or_tab_normal_pair_f.restype = None
+            lib.or_tab_normal_pair_f.argtypes = [_u32, _u32, _vp]
         getattr(lib, f"or_uniform_co_{sfx}").restype = rt
         getattr(lib, f"or_uniform_co_{sfx}").argtypes = [_u64, _u32, _u64, _u32, _u32]
         getattr(lib, f"or_logp_grad_{sfx}").restype = rt

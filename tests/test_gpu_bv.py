@@ -49,7 +49,7 @@ def test_random_fills_and_ln_match_oracle(bv, oracle, dtype):
     z = bv.DeviceMatrix((C, D), dtype)
     bv.fill_random_normal(z, seed, step, chain_offset=off)
     sfx = "f" if dtype == np.float32 else "d"
-    nrm = getattr(oracle.lib, f"or_normal_{sfx}")
+    nrm = getattr(oracle.lib, f"or_mom_normal_{sfx}")  # the HMC momentum draws (f32: spec v5 tables)
     exp = np.array([[nrm(seed, off + c, step, 2, j) for j in range(D)] for c in range(C)], dtype=dtype)
     np.testing.assert_array_equal(z.to_host(), exp)
     u = bv.sample_uniform(C, dtype, seed, step, chain_offset=off)

@@ -87,6 +87,33 @@ def test_tab_normal_pairs_and_moments(oracle):
     assert np.all(np.isfinite(z))
 
 
+def test_tab_normal_f32_momenta(oracle):
+    """Spec v5 for the f32 HMC momenta: table-driven pairs over the 4 words of
+    a block (steps 4k..4k+3), within 1.5e-6 of the exact Box-Muller value of
+    the same uniforms (a few f32 ulps of the radius), the msun f32 form's
+    pairs to the same accuracy, N(0, 1) moments; u1 = 1 gives (+0, +0)."""
+    import ctypes as C
+    import math
+    lib = oracle.lib
+    z = np.array([[lib.or_mom_normal_f(7, c, s, 2, d) for s in range(8)] for c in range(60) for d in range(50)])
+    msun = np.array([[lib.or_normal_f(7, c, s, 2, d) for s in range(8)] for c in range(60) for d in range(50)])
+    assert np.max(np.abs(z - msun)) < 2e-6
+    zz = z.ravel()
+    assert abs(zz.mean()) < 0.02 and abs(zz.std() - 1) < 0.02
+    assert abs(np.mean(zz ** 3)) < 0.1 and abs(np.mean(zz ** 4) - 3) < 0.3
+    out = (C.c_float * 2)()
+    rng = np.random.default_rng(3)
+    for w1, w2 in rng.integers(0, 2 ** 32, size=(4000, 2), dtype=np.uint64):
+        lib.or_tab_normal_pair_f(int(w1), int(w2), out)
+        u1, u2 = ((int(w1) >> 8) + 1) * 2.0 ** -24, (int(w2) >> 8) * 2.0 ** -24
+        r = math.sqrt(-2.0 * math.log(u1))
+        assert abs(out[0] - r * math.cos(2 * math.pi * u2)) < 1.5e-6
+        assert abs(out[1] - r * math.sin(2 * math.pi * u2)) < 1.5e-6
+    for w2 in (0, 0x12345678, 0xFFFFFFFF):
+        lib.or_tab_normal_pair_f(0xFFFFFFFF, w2, out)
+        assert out[0] == 0.0 and out[1] == 0.0
+
+
 def test_tab_normal_u1_one_is_zero(oracle):
     """u1 = 1 (all-ones words, probability 2^-53): the table form's ln u1
     rounds to +1.6e-17, so -2 ln u1 < 0; the clamp makes the pair exactly

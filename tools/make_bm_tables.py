@@ -1,16 +1,21 @@
-"""Tables of the table-driven f64 Box-Muller (RNG spec v5, the f64 MH proposal
-normals): 128 (1/c_j, ln c_j) pairs, c_j = 1 + (j + 1/2)/128, for
-ln m = ln c_j + ln(1 + (m/c_j - 1)) on m in [1, 2); 256 (sin, cos)(2 pi j/256)
-pairs for the angle-addition sin/cos. Written as C initializers (hex
-literals): the kernel (gm_bm_tables.h) and the oracle hold the same data.
+"""Tables of the table-driven Box-Muller (RNG spec v5: the f64 MH proposal
+normals and the f32 HMC momenta): 128 (1/c_j, ln c_j) pairs,
+c_j = 1 + (j + 1/2)/128, for ln m = ln c_j + ln(1 + (m/c_j - 1)) on m in
+[1, 2); 256 (sin, cos)(2 pi j/256) pairs for the angle-addition sin/cos. The
+f32 tables hold 1/c_j rounded to f32 and ln of the reciprocal of THAT value
+(so m * (1/c_j) - 1 stays the exact residual of the f32 factor), and sin/cos
+rounded to f32. Written as C initializers (hex literals): the kernel
+(gm_bm_tables.h) and the oracle hold the same data.
 
     python tools/make_bm_tables.py > general-mcmc_amd/csrc/gm_bm_tables.h
 """
 import math
 
+import numpy as np
+
 
 def main():
-    print("// gm_bm_tables.h -- tables of the f64 table-driven Box-Muller (RNG spec v5),")
+    print("// gm_bm_tables.h -- tables of the table-driven Box-Muller (RNG spec v5),")
     print("// written by tools/make_bm_tables.py; oracle/gm_bm_tables.h is the same file.")
     print("#pragma once")
     lg = []
@@ -34,6 +39,17 @@ def main():
     for k in range(0, len(sc), 4):
         print("  " + ", ".join(float(v).hex() for v in sc[k:k + 4]) + (", \\" if k + 4 < len(sc) else " \\"))
     print("")
+    lg32 = []
+    for j in range(128):
+        ic = np.float32(1.0 / (1.0 + (j + 0.5) / 128.0))
+        lg32 += [ic, np.float32(-math.log(float(ic)))]
+    sc32 = [np.float32(v) for v in sc]
+    for name, vals in (("GM_BM32_LOG_INIT", lg32), ("GM_BM32_SINCOS_INIT", sc32)):
+        print(f"#define {name} \\")
+        for k in range(0, len(vals), 4):
+            print("  " + ", ".join(float(v).hex() + "f" for v in vals[k:k + 4]) +
+                  (", \\" if k + 4 < len(vals) else " \\"))
+        print("")
 
 
 if __name__ == "__main__":
