@@ -87,6 +87,10 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
     }
   };
   const uint64_t st_end = a.step0 + (uint64_t)a.n_steps;
+  // this lane's first sample slot; each stored transition advances it one row
+  // (C*D elements) instead of recomputing the 64-bit row address
+  T* __restrict__ out = (T*)a.samples + (a.sample_row0 * a.C + c) * D + lane * E;
+  const long long row_stride = a.C * D;
 
   for (int s = 0; s < a.n_steps; ++s) {
     const uint64_t st = a.step0 + (uint64_t)s;
@@ -209,12 +213,12 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
       ++acc;
     }
     if (s >= a.collect_from) {
-      T* __restrict__ out = (T*)a.samples + ((a.sample_row0 + (s - a.collect_from)) * a.C + c) * D;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int i = lane * E + e;
-        if (i < D) out[i] = q[e];
+        if (i < D) out[e] = q[e];
       }
+      out += row_stride;
     }
   }
 #pragma unroll
