@@ -64,3 +64,23 @@ def test_rosenbrock_grad_central_differences(oracle, lay):
         lp_m, _ = oracle.logp_grad(t, xm, lanes, elems, np.float64)
         fd[:, i] = (lp_p - lp_m) / (2 * h)
     np.testing.assert_allclose(g, fd, rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype,tol", [(np.float64, 1e-11), (np.float32, 2e-4)])
+def test_hmc_leapfrog_forms_agree_to_rounding(oracle, dtype, tol):
+    """The oracle's two HMC leapfrog forms: 0, the engine's (kicks and drift
+    as fused multiply-adds, the kernels), and 1, the reference's op structure
+    (product and sum rounded separately, batched_hmc.rs:166-190 through
+    add_scaled_assign, the composed tier-2 ops). The same integrator in exact
+    arithmetic: one transition's proposals agree to rounding, and over a run
+    the accept rates match."""
+    C_, D, L = 32, 64, 20
+    x0 = (np.random.default_rng(4).standard_normal((C_, D)) * 0.5).astype(dtype)
+    t = Target(1, D, a=1.0, b=100.0)
+    _, s0, _ = oracle.hmc_run(t, x0, 0.005, L, 3, 0, 1, 0, 64, 1, form=0)
+    _, s1, _ = oracle.hmc_run(t, x0, 0.005, L, 3, 0, 1, 0, 64, 1, form=1)
+    assert not np.array_equal(s0, s1)  # the roundings differ ...
+    np.testing.assert_allclose(s0, s1, rtol=tol, atol=tol)  # ... and nothing else
+    _, _, a0 = oracle.hmc_run(t, x0, 0.005, L, 3, 0, 40, 40, 64, 1, form=0)
+    _, _, a1 = oracle.hmc_run(t, x0, 0.005, L, 3, 0, 40, 40, 64, 1, form=1)
+    assert abs(a0.mean() - a1.mean()) < 2.0  # of 40 transitions per chain
