@@ -118,7 +118,8 @@ __device__ __forceinline__ void packed_cols(const unsigned (&aA)[E], const unsig
         // p = L z skips the terms j > r (L_rj = 0); adding 0 * z_j = +-0 to
         // the +0-started sum changes no bit either
         const T mm = (CHOL && J + u > r[e]) ? (T)0 : m[u][e];
-        acc[e] = acc[e] + mm * pj[u];
+        if constexpr (CHOL) acc[e] = acc[e] + mm * pj[u];
+        else acc[e] = gfma(mm, pj[u], acc[e]);  // M^-1 p: the engine's fma chain (oracle inv_mul)
       }
     }
     packed_cols<LPC, E, T, J + NB, CHOL>(aA, aB, r, p, acc);
@@ -144,7 +145,7 @@ __device__ __forceinline__ void full_cols(unsigned base, const T (&p)[E], T (&ac
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) acc[e] = acc[e] + m[u][e] * pj[u];
+      for (int e = 0; e < E; ++e) acc[e] = gfma(m[u][e], pj[u], acc[e]);
     }
     full_cols<LPC, E, T, J + NB>(base, p, acc);
   }
@@ -249,7 +250,7 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E, K>& M, const T (&p)[
         if (j0 + u < M.D) {
 #pragma unroll
           for (int e = 0; e < E; ++e)
-            if (lane * E + e < M.D) acc[e] = acc[e] + mv[u][e] * pv[u];
+            if (lane * E + e < M.D) acc[e] = gfma(mv[u][e], pv[u], acc[e]);
         }
       }
     }
