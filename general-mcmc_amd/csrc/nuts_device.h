@@ -847,6 +847,9 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   T p0[E];               // the transition's momentum (starting chains)
   T qe[E], pe[E], ge[E];  // edge: the trajectory end on side v (being integrated)
   T qf[E], pf[E], gf[E];  // the far end
+  // dense metric: M^-1 p and M^-1 g of both ends, carried by linearity
+  // (carried_velocity below); the start's M^-1 p0
+  T ve[E], we[E], vf[E], wf[E], v0[E];
   int v = 1, j = 0;
   // tree counts fit 32 bits: the depth cap (<= NUTS_MAX_DEPTH_LIMIT = 30) bounds n by 2^30
   int l = 0, n = 1;
@@ -860,6 +863,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     qe[e] = pe[e] = ge[e] = qf[e] = pf[e] = gf[e] = fq[e] = fp[e] = pr[e] = p0[e] = (T)0;
+    ve[e] = we[e] = vf[e] = wf[e] = v0[e] = (T)0;
   }
 
 #ifdef GM_NUTS_PROF
@@ -936,13 +940,23 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
         pe[e] = pe[e] + ge[e] * h;
         qe[e] = qe[e] + pe[e] * epsv;
       }
-    } else if (live && !starting) {  // leapfrog_with_mass (:1396-1418): kick, drift by M^-1 p
+    }
+    // the drift's M^-1 p (the kicked momentum); with a dense metric carried
+    // from the edge: M^-1 (p + g h) = M^-1 p + (M^-1 g) h
+    T vv[E];
+    if constexpr (MASS != 0) {
+      if (live && !starting) {  // leapfrog_with_mass (:1396-1418): kick, drift by M^-1 p
 #pragma unroll
-      for (int e = 0; e < E; ++e) pe[e] = pe[e] + ge[e] * h;
-      T vv[E];
-      inv_mul<LPC, E>(M, pe, vv, lane);
+        for (int e = 0; e < E; ++e) pe[e] = pe[e] + ge[e] * h;
+        if (MASS == 2 && M.kind() == 2) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) qe[e] = qe[e] + vv[e] * epsv;
+          for (int e = 0; e < E; ++e) vv[e] = ve[e] + we[e] * h;
+        } else {
+          inv_mul<LPC, E>(M, pe, vv, lane);
+        }
+#pragma unroll
+        for (int e = 0; e < E; ++e) qe[e] = qe[e] + vv[e] * epsv;
+      }
     }
 #pragma unroll
     for (int e = 0; e < E; ++e) x[e] = starting ? q[e] : qe[e];
@@ -956,11 +970,35 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
 #endif
 #pragma unroll
     for (int e = 0; e < E; ++e) pe[e] = pe[e] + gx[e] * h;  // (unconditionally, as above)
+    T wx[E];  // dense metric: M^-1 g at the evaluation point
     {
       T pk[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) pk[e] = starting ? p0[e] : pe[e];
-      sums[1] = kin_part_m<LPC, E>(M, pk, lane);
+      if constexpr (MASS == 2) {
+        // carried_velocity: one product per evaluation (M^-1 g) instead of
+        // two (the drift's M^-1 p and the kinetic energy's); a starting
+        // chain's M^-1 p0 only in iterations where some chain of the wave
+        // starts a transition
+        inv_mul<LPC, E>(M, gx, wx, lane);
+        if (__builtin_amdgcn_ballot_w64(live && starting && M.kind() == 2) != 0) inv_mul<LPC, E>(M, p0, v0, lane);
+        if (M.kind() == 2) {
+          T t[E];
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            vv[e] = starting ? v0[e] : vv[e] + wx[e] * h;  // M^-1 p at the evaluation point
+            t[e] = pk[e] * vv[e];
+          }
+          T part = t[0];
+#pragma unroll
+          for (int e = 1; e < E; ++e) part = part + t[e];
+          sums[1] = part;
+        } else {
+          sums[1] = kin_part_m<LPC, E>(M, pk, lane);
+        }
+      } else {
+        sums[1] = kin_part_m<LPC, E>(M, pk, lane);
+      }
     }
 #ifdef GM_NUTS_PROF
     GM_PSEG(3);
@@ -994,6 +1032,13 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
         qe[e] = q[e]; pe[e] = p0[e]; ge[e] = gx[e];
         qf[e] = q[e]; pf[e] = p0[e]; gf[e] = gx[e];
       }
+      if constexpr (MASS == 2) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          ve[e] = v0[e]; we[e] = wx[e];
+          vf[e] = v0[e]; wf[e] = wx[e];
+        }
+      }
       n = 1;
       j = 0;
       l = 0;
@@ -1007,6 +1052,10 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     ++nlf;
 #pragma unroll
     for (int e = 0; e < E; ++e) ge[e] = gx[e];
+    if constexpr (MASS == 2) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) { ve[e] = vv[e]; we[e] = wx[e]; }
+    }
     const T joint = lp - kin;
     tn = (logu < joint) ? 1 : 0;
     ts = (logu - (T)1000) < joint;
@@ -1091,8 +1140,11 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       {
         // the trajectory's ends: the edge (qe, pe) on side v and the far end
         // (qf, pf), unordered (no_uturn_ends)
-        if constexpr (MASS == 2) {  // the dense products: only where needed
-          if (s_ok) s_ok = no_uturn_ends_m<LPC, E>(M, qe, qf, pe, pf, v, lane);
+        if constexpr (MASS == 2) {  // dense: the ends' carried M^-1 p (no product)
+          if (s_ok) {
+            if (M.kind() == 2) s_ok = no_uturn_ends<LPC, E>(qe, qf, ve, vf, v);
+            else s_ok = no_uturn_ends_m<LPC, E>(M, qe, qf, pe, pf, v, lane);
+          }
         } else {
           const bool nu = no_uturn_ends_m<LPC, E>(M, qe, qf, pe, pf, v, lane);
           s_ok = s_ok && nu;
@@ -1111,6 +1163,16 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
           qf[e] = sw ? a0 : qf[e];
           pf[e] = sw ? a1 : pf[e];
           gf[e] = sw ? a2 : gf[e];
+        }
+        if constexpr (MASS == 2) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            const T b0 = ve[e], b1 = we[e];
+            ve[e] = sw ? vf[e] : ve[e];
+            we[e] = sw ? wf[e] : we[e];
+            vf[e] = sw ? b0 : vf[e];
+            wf[e] = sw ? b1 : wf[e];
+          }
         }
         v = v2;
         l = 0;

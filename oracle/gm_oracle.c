@@ -846,7 +846,7 @@ void or_build_tree_d(const or_target* t, int lanes, int elems, const double* q, 
   cx.tmpv2 = (double*)malloc(sizeof(double) * D);
   tree_d out;
   tree_alloc_d(&out, D);
-  build_tree_d(&cx, q, p, g, logu, v, j, eps, joint0, &out);
+  build_tree_d(&cx, q, p, g, NULL, NULL, logu, v, j, eps, joint0, &out);  /* identity mass */
   const double* vs[8] = {out.qm, out.pm, out.gm, out.qp, out.pp, out.gp, out.qprime, out.gprime};
   for (int k = 0; k < 8; ++k) memcpy(out_vecs + k * D, vs[k], sizeof(double) * D);
   out_scalars[0] = out.logp_prime;
