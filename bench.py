@@ -648,10 +648,12 @@ def config_summary(name, cfg, figs, world, rhat, ess):
         t_w = max(f.get("warmup_s", 0.0) for f in figs)
         n_samp = cfg["n_collect"] - 1
         # the target's GEMV and the kicks/drift, 2D^2 + 8D; under
-        # a dense metric each leaf adds two M^-1 products (the drift's and the
-        # kinetic energy's, generic_nuts.rs:255-273, 1396-1418), 2D^2 each (the
-        # products at doubling ends and transition starts are not counted)
-        fa = 2 * D * D + 8 * D + (4 * D * D if cfg.get("mass") == "dense" else 0)
+        # a dense metric each leaf adds the ONE M^-1 product the engine does
+        # (of the new gradient: M^-1 p is carried by linearity, DESIGN.md §3,
+        # where the reference's formulation takes two, generic_nuts.rs:255-273,
+        # 1396-1418) and the carried velocity's 4D (the products at transition
+        # starts are not counted)
+        fa = 2 * D * D + 8 * D + (2 * D * D + 4 * D if cfg.get("mass") == "dense" else 0)
         tf = fa * (lf / world) / (kms * 1e-3) / 1e12
         mass = f", {cfg['mass']} mass-matrix adaptation" if cfg.get("mass") else ""
         out.update(workload=f"NUTS DenseGaussian dim={D} f64, {chains} chains, target_accept "
@@ -667,9 +669,9 @@ def config_summary(name, cfg, figs, world, rhat, ess):
                    roofline={"bound": "valu_f64", "kernel": "nuts_kernel", "achieved": tf,
                              "peak": VALU_F64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / VALU_F64_PEAK_TFLOPS,
                              "flops_per_leapfrog": fa,
-                             "note": "F = 2D^2 + 8D per leapfrog (SURVEY 8(d)), + 4D^2 for the two M^-1 "
-                                     "products of a leaf under a dense metric, x leapfrogs counted on the "
-                                     "device / the run's HIP-event kernel time (per GPU)"})
+                             "note": "F = 2D^2 + 8D per leapfrog (SURVEY 8(d)), + 2D^2 + 4D under a dense "
+                                     "metric (the leaf's one M^-1 product and the carried M^-1 p), x leapfrogs "
+                                     "counted on the device / the run's HIP-event kernel time (per GPU)"})
     elif cfg["kind"] == "hmc":
         work = chains * cfg["L"] * total
         fa = f_alg_rosenbrock(D)
