@@ -22,8 +22,9 @@ struct NutsState {
   int* stk_n = nullptr;       // [max_depth][C]
   int* stk_na = nullptr;      // [max_depth][C]
   long long lds_levels_cap = -1;  // subtree-stack levels in LDS: -1 as many as fit
-  int dense_minv_lds = 2;     // dense M^-1 in LDS when it fits: 2 full or packed, 1 packed only, 0 off
-  int dense_chol_lds = 1;     // its Cholesky factor too (packed form only)
+  int dense_minv_lds = 1;     // dense M^-1 in LDS: 1 packed (the default: room for 6 stack levels),
+                              // 2 full when it fits (else packed), 0 off
+  int dense_chol_lds = 0;     // its Cholesky factor too (packed form only)
   int plan[5] = {0, 0, 0, 0, 0};  // last launch: stack levels in LDS, M^-1 form, offset, L form, offset
   long long* n_leapfrog = nullptr;  // [C] cumulative leapfrog count
   long long m = 0;            // transitions since the last init_chain_state (:735)

@@ -1179,9 +1179,13 @@ int gm_nuts_set_dense_forms(gm_sampler* s, int32_t minv_lds, int32_t chol_lds) {
   GM_REQ(s, "sampler is NULL");
   GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");
   GM_REQ(minv_lds >= -1 && minv_lds <= 2, "minv_lds must be -1 (automatic), 0, 1 or 2");
-  GM_REQ(chol_lds == 0 || chol_lds == 1, "chol_lds must be 0 or 1");
-  s->nuts.dense_minv_lds = minv_lds < 0 ? 2 : minv_lds;
-  s->nuts.dense_chol_lds = chol_lds;
+  GM_REQ(chol_lds >= -1 && chol_lds <= 1, "chol_lds must be -1 (automatic), 0 or 1");
+  // automatic: the packed M^-1 in LDS and L in global memory, which leaves
+  // 6 subtree-stack levels on chip (HBM 3.2 GB per cfg3 sampling launch
+  // instead of 34.7 GB with the full matrices, 1.8 % slower:
+  // profiles/r04/dense_forms_carried.jsonl, dense_traffic.json)
+  s->nuts.dense_minv_lds = minv_lds < 0 ? 1 : minv_lds;
+  s->nuts.dense_chol_lds = chol_lds < 0 ? 0 : chol_lds;
   return GM_OK;
 }
 

@@ -17,9 +17,9 @@ struct NutsLdsBudget {
   int ncu = 256;                // compute units
   int lds_max = 64 * 1024;      // dynamic LDS per block
   long long lds_cap = -1;       // levels cap (-1: as many as fit)
-  int minv_lds = 2;             // dense metric in LDS when it fits: 2 full or packed, 1 packed only, 0 off
+  int minv_lds = 1;             // dense metric in LDS: 1 packed, 2 full when it fits (else packed), 0 off
                                 // (gm_nuts_set_dense_forms)
-  int chol_lds = 1;             // its Cholesky factor too (0: off)
+  int chol_lds = 0;             // its Cholesky factor too (0: off)
 };
 
 // LDS of a launch: the target's staging area (tgl bytes), then as many

@@ -103,10 +103,12 @@ class NUTS(Sampler):
         _lib.check(self._lib.gm_nuts_set_lds_levels(self._h, int(levels)))
         return self
 
-    def set_dense_forms(self, minv_lds: int = -1, chol_lds: int = 1):
+    def set_dense_forms(self, minv_lds: int = -1, chol_lds: int = -1):
         """Placement of the dense metric's matrices (gm_nuts_set_dense_forms):
-        minv_lds 2/-1 full-or-packed in LDS, 1 packed only, 0 global memory;
-        chol_lds 1 the packed Cholesky factor in LDS too. Identical results."""
+        minv_lds -1 automatic (= 1), 1 the packed triangle in LDS, 2 the full
+        matrix when it fits (else packed), 0 global memory; chol_lds -1
+        automatic (= 0), 1 the packed Cholesky factor in LDS too. Identical
+        results."""
         _lib.check(self._lib.gm_nuts_set_dense_forms(self._h, int(minv_lds), int(chol_lds)))
         return self
 

@@ -232,12 +232,14 @@ int gm_nuts_set_mass_adaptation(gm_sampler* s, int32_t mode, int64_t start_buffe
 int gm_nuts_set_lds_levels(gm_sampler* s, int32_t levels);
 
 /* Where a dense-metric NUTS sampler (layout 16 x 2, dim <= 32) keeps each
- * chain's M^-1 and Cholesky factor: minv_lds 2 (the default, also -1) the
- * full matrices in LDS when they fit next to the target's staging, else the
- * packed lower triangles; 1 packed triangles only; 0 global memory.
- * chol_lds 1 also packs the Cholesky factor into LDS when the packed M^-1
- * leaves room. Every form gives identical results (no reference
- * counterpart: a placement choice of this engine). */
+ * chain's M^-1 and Cholesky factor: minv_lds 1 (the default, also -1) the
+ * packed lower triangles in LDS, which leaves room for 6 subtree-stack
+ * levels on chip; 2 the full matrices when they fit next to the target's
+ * staging (else packed: one stack level, ~10x the HBM traffic, ~2 % faster);
+ * 0 global memory. chol_lds 1 also packs the Cholesky factor into LDS when
+ * the packed M^-1 leaves room (default, also -1: 0). Every form gives
+ * identical results (no reference counterpart: a placement choice of this
+ * engine). */
 int gm_nuts_set_dense_forms(gm_sampler* s, int32_t minv_lds, int32_t chol_lds);
 
 /* The last NUTS launch's on-chip plan: plan[0] subtree-stack levels in LDS,

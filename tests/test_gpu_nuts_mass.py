@@ -87,7 +87,7 @@ def test_dense_warmup_wide_layout(gm, oracle):
                    initial_window=10)
 
 
-@pytest.mark.parametrize("minv_lds,chol_lds", [("2", "1"), ("1", "1"), ("1", "0"), ("0", "0")])
+@pytest.mark.parametrize("minv_lds,chol_lds", [("2", "1"), ("1", "1"), ("1", "0"), ("0", "0"), ("-1", "-1")])
 @pytest.mark.parametrize("D,chains", [(20, 10), (32, 36)])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 def test_dense_warmup_matrix_core_layout(gm, oracle, minv_lds, chol_lds, D, chains, dtype):
@@ -95,10 +95,12 @@ def test_dense_warmup_matrix_core_layout(gm, oracle, minv_lds, chol_lds, D, chai
     on the matrix cores for f64) with each form of the dense metric's
     products: M^-1 full in LDS (2), its packed lower triangle with or without
     the packed Cholesky factor (1), and the transposed per-chain matrices in
-    global memory (0) (gm_nuts_set_dense_forms, nuts_launch.h); D = 20 pads
-    rows and columns to 32, and 10 or 36 chains leave the last wave partly
-    empty (the VALU target product there). The launch plan read back shows
-    the form actually used."""
+    global memory (0), and the automatic choice (-1: the packed M^-1 with L
+    in global memory, which leaves several subtree-stack levels in LDS)
+    (gm_nuts_set_dense_forms, nuts_launch.h); D = 20 pads rows and columns
+    to 32, and 10 or 36 chains leave the last wave partly empty (the VALU
+    target product there). The launch plan read back shows the form actually
+    used."""
     rng = np.random.default_rng(21)
     a = rng.standard_normal((D, D))
     cov = a @ a.T / D + 0.5 * np.eye(D)
@@ -110,6 +112,9 @@ def test_dense_warmup_matrix_core_layout(gm, oracle, minv_lds, chol_lds, D, chai
     assert s.layout() == (16, 2)
     assert np.any(om.kind == 2)
     plan = s.launch_plan()
+    if minv_lds == "-1":
+        assert plan["minv_lds"] == 1 and plan["chol_lds"] == 0 and plan["lds_levels"] >= 4, plan
+        return
     assert plan["minv_lds"] == int(minv_lds) or (minv_lds == "2" and plan["minv_lds"] == 1)
     assert plan["chol_lds"] <= int(chol_lds) and (plan["chol_lds"] == 0 or plan["minv_lds"] == 1)
 
