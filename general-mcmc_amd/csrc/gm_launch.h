@@ -33,7 +33,7 @@ struct HmcLaunch {
   int n_steps = 0;
   int collect_from = 0;         // steps s >= collect_from are stored ...
   long long sample_row0 = 0;    // ... at row sample_row0 + (s - collect_from)
-  int lf_unroll = 1;            // leapfrog loop unroll (1 or 4; same results)
+  int lf_unroll = 1;            // leapfrog loop unroll (1, 2 or 4; same results)
   void* zs = nullptr;           // wide layouts: momentum block scratch [C][S][lanes*elems]
 };
 

@@ -688,7 +688,9 @@ static int hmc_lf_unroll(long long waves) {
       cus = 256;
     return 4 * cus;
   }();
-  return waves <= simds ? 4 : 1;
+  // x4 at <= 1 wave per SIMD, x2 at <= 4 (the cfg2 headline), x1 above
+  // (cfg4's 8 and the north star's 16 waves per SIMD), measured per regime
+  return waves <= simds ? 4 : waves <= 4 * simds ? 2 : 1;
 }
 
 // hipSetDevice only when the calling thread is on another device (the call

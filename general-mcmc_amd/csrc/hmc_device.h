@@ -157,6 +157,11 @@ __global__ __launch_bounds__(256) void hmc_kernel(HmcLaunch a, TG tg_) {
     int l = 0;
     if (a.lf_unroll == 4)
       for (; l + 4 < a.L; l += 4) { lf(); lf(); lf(); lf(); }
+    // two leapfrogs per loop trip at 2-4 waves per SIMD (one taken branch and
+    // loop test per two): kernel -1.4 % at the headline's 4 waves per SIMD,
+    // but cfg4 at 8 waves per SIMD -4.7 % (profiles/r04/ab_hmc_unroll2.log)
+    if (a.lf_unroll == 2)
+      for (; l + 2 < a.L; l += 2) { lf(); lf(); }
     for (; l + 1 < a.L; ++l) lf();
     // 6. proposed kinetic energy, from the in-lane sums of p'^2
     auto kin_part = [&]() __attribute__((always_inline)) {
