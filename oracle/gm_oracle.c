@@ -494,7 +494,7 @@ int or_mass_diag_kat(const double* var, int D, double jitter, const double* p, d
   for (int i = 0; i < D; ++i) q = q + p[i] * p[i] * inv[i];
   *ke = 0.5 * q;
   mass_d M = {1, inv, sq, NULL};
-  inv_mul_d(&M, p, inv_mul_out, D);
+  inv_mul_d(&M, p, inv_mul_out, D, 1);  /* the reference's two roundings */
   return 0;
 }
 
@@ -503,7 +503,7 @@ int or_mass_dense_kat(const double* cov, int D, double jitter, const double* p, 
   if (D > 64) return 1;
   if (!dense_from_cov_d(cov, D, jitter, inv, chol)) return 2;
   mass_d M = {2, inv, NULL, chol};
-  inv_mul_d(&M, p, inv_mul_out, D);
+  inv_mul_d(&M, p, inv_mul_out, D, 1);  /* the reference's two roundings */
   return 0;
 }
 

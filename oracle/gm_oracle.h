@@ -128,6 +128,9 @@ typedef struct or_mass_cfg {
   int mode; /* 0 none, 1 diagonal, 2 dense (dense_max_dim already applied) */
   int64_t start_buffer, end_buffer, initial_window;
   double regularize, jitter;
+  int form; /* NUTS arithmetic: 0 the engine's (the kernels, bitwise), 1 the reference's op
+             * structure (generic_nuts.rs:227-276, 1357-1418: fresh M^-1 products with two
+             * roundings, left-to-right kinetic sums) */
 } or_mass_cfg;
 typedef struct or_mass_state {
   int32_t* kind;     /* [C]: 0 identity, 1 diagonal, 2 dense */
@@ -151,6 +154,17 @@ int or_nuts_mass_run_f(const or_target* t, int lanes, int elems, int64_t C, int 
                        int64_t n_collect, int64_t n_discard, int progress, float* samples,
                        int64_t* accepts, int64_t* n_leapfrog, const or_mass_cfg* cfg,
                        or_mass_state* ms, int threads);
+/* A trajectory of n_leap leapfrogs under a dense metric M^-1 = inv [D][D]
+ * from (q, p), in either form: 0 the engine's (M^-1 p and M^-1 g carried by
+ * linearity, fma-chain products, canonical-order kinetic sum), 1 the
+ * reference's leapfrog_with_mass / kinetic (generic_nuts.rs:1396-1418,
+ * 227-276). q, p are updated in place; vel = M^-1 p at the end (form 0 the
+ * carried value, form 1 a fresh product); out[0] = logp, out[1] = kinetic.
+ * Returns 0 on success. */
+int or_dense_traj_d(const or_target* t, int lanes, int elems, int D, const double* inv, double* q,
+                    double* p, double eps, int n_leap, int form, double* vel, double* out);
+int or_dense_traj_f(const or_target* t, int lanes, int elems, int D, const float* inv, float* q,
+                    float* p, double eps, int n_leap, int form, float* vel, float* out);
 /* the reference's MassMatrix unit tests (generic_nuts.rs:1427-1489):
  * diagonal_from_var -> kinetic / inv_mul; dense_from_cov -> inv_mul;
  * RunningCov + maybe_update_mass_matrix (diagonal). Return 0 on success. */

@@ -76,6 +76,9 @@ def load():
         getattr(lib, f"or_nuts_mass_run_{sfx}").argtypes = [
             tp, _int, _int, _i64, _int, _vp, _vp, _vp, _vp, _vp, _dbl, _int, _u64, _u64, _u32, _i64,
             _i64, _int, _vp, _vp, _vp, C.POINTER(or_mass_cfg), C.POINTER(or_mass_state), _int]
+    for sfx in ("d", "f"):
+        getattr(lib, f"or_dense_traj_{sfx}").argtypes = [tp, _int, _int, _int, _vp, _vp, _vp, _dbl, _int,
+                                                         _int, _vp, _vp]
     lib.or_mass_state_init.argtypes = [C.POINTER(or_mass_cfg), _i64, _int, _int, C.POINTER(or_mass_state)]
     lib.or_mass_diag_kat.argtypes = [_vp, _int, _dbl, _vp, _vp, _vp]
     lib.or_mass_dense_kat.argtypes = [_vp, _int, _dbl, _vp, _vp]
@@ -129,7 +132,8 @@ def cpu_hmc():
 
 class or_mass_cfg(C.Structure):
     _fields_ = [("mode", C.c_int), ("start_buffer", C.c_int64), ("end_buffer", C.c_int64),
-                ("initial_window", C.c_int64), ("regularize", C.c_double), ("jitter", C.c_double)]
+                ("initial_window", C.c_int64), ("regularize", C.c_double), ("jitter", C.c_double),
+                ("form", C.c_int)]
 
 
 class or_mass_state(C.Structure):
@@ -141,8 +145,10 @@ class NutsMass:
     """Host arrays of the oracle's per-chain mass state (or_mass_state)."""
 
     def __init__(self, lib, mode, C_, D, dtype, start_buffer=75, end_buffer=50, initial_window=25,
-                 regularize=0.05, jitter=1e-6):
-        self.cfg = or_mass_cfg(mode, start_buffer, end_buffer, initial_window, regularize, jitter)
+                 regularize=0.05, jitter=1e-6, form=0):
+        # form 0: the engine's arithmetic (the kernels' bits); 1: the
+        # reference's op structure (fresh M^-1 products, two roundings)
+        self.cfg = or_mass_cfg(mode, start_buffer, end_buffer, initial_window, regularize, jitter, form)
         self.kind = np.zeros(C_, dtype=np.int32)
         self.dinv = np.zeros((C_, D), dtype=dtype)
         self.dsqrt = np.zeros((C_, D), dtype=dtype)
@@ -329,6 +335,22 @@ class Oracle:
             C.byref(mass.cfg), C.byref(mass.st), threads)
         assert rc == 0
         return q, samples, acc, nlf
+
+    def dense_traj(self, target: Target, inv, q, p, eps, n_leap, form, lanes, elems):
+        """n_leap leapfrogs under the dense metric M^-1 = inv from (q, p) in
+        the engine's form (0) or the reference's (1): (q, p, M^-1 p, logp,
+        kinetic)."""
+        dt = np.asarray(q).dtype
+        q = np.array(q, dtype=dt, copy=True)
+        p = np.array(p, dtype=dt, copy=True)
+        inv = np.ascontiguousarray(inv, dtype=dt)
+        vel = np.zeros_like(q)
+        out = np.zeros(2, dtype=dt)
+        t = target.struct()
+        rc = getattr(self.lib, f"or_dense_traj_{_sfx(dt)}")(C.byref(t), lanes, elems, q.shape[0], _p(inv), _p(q),
+                                                             _p(p), eps, n_leap, form, _p(vel), _p(out))
+        assert rc == 0
+        return q, p, vel, out[0], out[1]
 
     def mct_p_accept(self, steps):
         """MultiChainTracker acceptance EMA after stepping [nsteps, C, P]."""
