@@ -95,6 +95,7 @@ SIGNATURES = {
     "gm_sampler_set_layout": (_ip, [_vp, _i32, _i32]),
     "gm_sampler_last_run_stats": (_ip, [_vp, C.POINTER(_dbl), C.POINTER(_i64)]),
     "gm_sampler_set_steps_per_launch": (_ip, [_vp, _i64]),
+    "gm_sampler_set_unroll": (_ip, [_vp, _i32]),
     "gm_sampler_set_async": (_ip, [_vp, _i32]),
     "gm_sampler_synchronize": (_ip, [_vp]),
     "gm_sampler_reserve": (_ip, [_vp, _i64]),

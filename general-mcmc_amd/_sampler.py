@@ -217,6 +217,11 @@ class Sampler:
         _lib.check(self._lib.gm_sampler_set_steps_per_launch(self._h, n))
         return self
 
+    def set_unroll(self, n: int):
+        """HMC leapfrog-loop unroll: 0 automatic, or 1, 2, 4 (same results)."""
+        _lib.check(self._lib.gm_sampler_set_unroll(self._h, int(n)))
+        return self
+
     def save_state(self) -> bytes:
         """Checkpoint (gm_state_save): positions, counters, seed and stream
         position, NUTS adaptation and metric. The reference has none

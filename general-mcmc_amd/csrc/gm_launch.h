@@ -114,6 +114,20 @@ struct NutsLaunch {
   long long sb = 0, eb = 0;  // start_buffer, end_buffer (should_collect, :153-162)
   int do_refind = 0;         // re-find eps for updated chains first (:905-918)
   uint64_t refind_step = 0;  // transition index of the update (probe draws)
+  // every chain's metric dense and no warm-up window in this launch: the
+  // frozen-dense instantiation (nuts_device.h MASS 3, GM_FROZEN_WAVES waves
+  // per SIMD) instead of the general adaptive one
+  int dense_frozen = 0;
 };
+
+// waves per SIMD of the NUTS dense-metric instantiations (their launch
+// bounds, which the LDS plan of nuts_size_lds follows): the adaptive one
+// (MASS 2) at 512 registers, the frozen one (MASS 3)
+#ifndef GM_DENSE_WAVES
+#define GM_DENSE_WAVES 1
+#endif
+#ifndef GM_FROZEN_WAVES
+#define GM_FROZEN_WAVES 2
+#endif
 
 }  // namespace gm

@@ -52,9 +52,12 @@ hipError_t dispatch_target(const TargetDev& tg, F& f) {
       t.prec = (const T*)tg.prec;
       t.nc = (T)tg.norm_const;
       t.D = tg.D;
-      // LDS staging while it leaves room for >= 4 blocks (16 waves) per CU,
+      // LDS staging while it leaves room for >= 4 blocks (16 waves) per CU
+      // next to the kernels' static Box-Muller tables (gm_rng.h: BmLds32,
+      // 3 KiB, in the f32 HMC kernels; BmLds, 6 KiB, in the f64 MH kernel),
       // or for the matrix-core form (f64 16 x 4 at D <= 64: 41 KiB)
-      t.use_lds = GaussT<T>::template lds_need<LPC, E>(tg.D) <= 40 * 1024 ||
+      constexpr size_t bm_static = sizeof(T) == 4 ? 3 * 1024 : 6 * 1024;
+      t.use_lds = GaussT<T>::template lds_need<LPC, E>(tg.D) <= 40 * 1024 - bm_static ||
                   (GaussT<T>::template mfma_form<LPC, E>() && tg.D <= 16 * E);
       return f.template operator()<T, LPC, E>(t);
     }

@@ -25,7 +25,7 @@ struct NutsState {
   int dense_minv_lds = 1;     // dense M^-1 in LDS: 1 packed (the default: room for 6 stack levels),
                               // 2 full when it fits (else packed), 0 off
   int dense_chol_lds = 0;     // its Cholesky factor too (packed form only)
-  int plan[5] = {0, 0, 0, 0, 0};  // last launch: stack levels in LDS, M^-1 form, offset, L form, offset
+  int plan[6] = {0, 0, 0, 0, 0, 0};  // last launch: stack levels in LDS, M^-1 form, offset, L form, offset, frozen
   long long* n_leapfrog = nullptr;  // [C] cumulative leapfrog count
   long long m = 0;            // transitions since the last init_chain_state (:735)
   long long n_discard = 0;    // warm-up length of the current run (:734)

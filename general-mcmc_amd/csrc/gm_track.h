@@ -48,6 +48,30 @@ template <int LPC, int E> struct ChainTrack {
     const float p_start = (p >= 0.0f) ? p : (first ? 1.0f : 0.0f);  // stats.rs:108-113
     p = (1.0f - 0.01f) * p_start + 0.01f * (any ? 1.0f : 0.0f);     // ALPHA = 0.01
   }
+  // the vectors alone (a kernel short of registers keeps them in memory
+  // between transitions: load_vec, step, store_vec; p stays in a register)
+  __device__ __forceinline__ void load_vec(const TrackLaunch& t, long long c, int lane, int D) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      const long long k = c * D + i;
+      m[e] = (i < D) ? t.mean[k] : 0.0f;
+      q[e] = (i < D) ? t.msq[k] : 0.0f;
+      l[e] = (i < D) ? t.last[k] : 0.0f;
+    }
+  }
+  __device__ __forceinline__ void store_vec(const TrackLaunch& t, long long c, int lane, int D) const {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int i = lane * E + e;
+      if (i < D) {
+        const long long k = c * D + i;
+        t.mean[k] = m[e];
+        t.msq[k] = q[e];
+        t.last[k] = l[e];
+      }
+    }
+  }
   __device__ __forceinline__ void store(const TrackLaunch& t, long long c, int lane, int D) const {
 #pragma unroll
     for (int e = 0; e < E; ++e) {

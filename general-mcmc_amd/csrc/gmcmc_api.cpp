@@ -199,6 +199,7 @@ struct gm_sampler {
   size_t zs_bytes = 0;
   Layout lay;
   long long steps_per_launch = 1000;
+  int lf_unroll = 0;  // HMC leapfrog-loop unroll: 0 by the wave count (hmc_lf_unroll), else 1, 2 or 4
   std::vector<hipEvent_t> evs;
   double last_ms = 0;
   long long last_launches = 0;
@@ -655,6 +656,13 @@ int gm_sampler_set_steps_per_launch(gm_sampler* s, int64_t steps) {
   return GM_OK;
 }
 
+int gm_sampler_set_unroll(gm_sampler* s, int32_t n) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(n == 0 || n == 1 || n == 2 || n == 4, "unroll must be 0 (automatic), 1, 2 or 4");
+  s->lf_unroll = n;
+  return GM_OK;
+}
+
 int gm_sampler_reserve(gm_sampler* s, int64_t n_collect) {
   GM_REQ(s, "sampler is NULL");
   GM_REQ(n_collect >= 0, "n_collect must be >= 0");
@@ -738,7 +746,8 @@ static int run_steps(gm_sampler* s, long long total, long long collect_from, int
   const long long n_launch = (total + chunk - 1) / chunk;
   int rc = ensure_run_events(s);
   if (rc) return rc;
-  const int lf_unroll = s->kind == K_HMC ? hmc_lf_unroll((s->C * s->lay.lanes + 63) / 64) : 1;
+  const int lf_unroll = s->kind != K_HMC ? 1 : s->lf_unroll ? s->lf_unroll
+                                                             : hmc_lf_unroll((s->C * s->lay.lanes + 63) / 64);
   for (long long start = 0; start < total; start += chunk) {
     LaunchEvents ev;  // start with the first launch, stop with the last
     if (start == 0) ev.start = s->evs[0];
@@ -1194,7 +1203,7 @@ int gm_nuts_set_dense_forms(gm_sampler* s, int32_t minv_lds, int32_t chol_lds) {
 int gm_nuts_get_plan(gm_sampler* s, int32_t* plan) {
   GM_REQ(s && plan, "NULL argument");
   GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");
-  for (int i = 0; i < 5; ++i) plan[i] = s->nuts.plan[i];
+  for (int i = 0; i < 6; ++i) plan[i] = s->nuts.plan[i];
   return GM_OK;
 }
 

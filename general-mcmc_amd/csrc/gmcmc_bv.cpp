@@ -67,11 +67,15 @@ int gm_memcpy_dtod(void* dst, const void* src, size_t bytes) {
   if ((((uintptr_t)dst | (uintptr_t)src | (uintptr_t)bytes) & 15) == 0) {
     int dev = -1;
     hipPointerAttribute_t as{}, ad{};
-    if (hipGetDevice(&dev) == hipSuccess && hipPointerGetAttributes(&as, src) == hipSuccess &&
-        hipPointerGetAttributes(&ad, dst) == hipSuccess && as.type == hipMemoryTypeDevice &&
-        ad.type == hipMemoryTypeDevice && as.device == dev && ad.device == dev)
+    const bool qd = hipGetDevice(&dev) == hipSuccess;
+    const bool qs = qd && hipPointerGetAttributes(&as, src) == hipSuccess;
+    const bool qt = qs && hipPointerGetAttributes(&ad, dst) == hipSuccess;
+    if (qt && as.type == hipMemoryTypeDevice && ad.type == hipMemoryTypeDevice && as.device == dev &&
+        ad.device == dev)
       return bv_status(launch_copy16(src, dst, (long long)(bytes / 16), nullptr), "copy16");
-    (void)hipGetLastError();  // a failed attribute query leaves no sticky error
+    // only a query that itself failed (e.g. host memory the runtime does not
+    // know) left an error to clear; an earlier pending error stays visible
+    if (!qt) (void)hipGetLastError();
   }
   return bv_status(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, nullptr), "hipMemcpy D2D");
 }

@@ -24,7 +24,9 @@ __device__ __forceinline__ T coord(const T (&x)[E], int j) {
 // the most general metric the kernel supports, known at compile time: 0 the
 // identity only (a sampler without mass-matrix adaptation: no metric branch
 // is emitted), 1 identity or diagonal (diagonal adaptation: no dense code),
-// 2 any (dense adaptation).
+// 2 any (dense adaptation), 3 every chain dense and the metric frozen for the
+// launch (dense adaptation past its last warm-up window: no identity or
+// diagonal branch, no Welford state; nuts_run picks it).
 template <class T, int E, int K = 2> struct MassDev {
   static constexpr bool DENSE = K >= 2;
   int kind_ = 0;            // 0 identity, 1 diagonal, 2 dense
@@ -37,7 +39,8 @@ template <class T, int E, int K = 2> struct MassDev {
   unsigned chol_off = 0;
   int D = 0;
   __device__ __forceinline__ int kind() const {
-    if constexpr (K > 0) return kind_;
+    if constexpr (K >= 3) return 2;
+    else if constexpr (K > 0) return kind_;
     else return 0;
   }
 };
@@ -222,6 +225,10 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E, K>& M, const T (&p)[
           r[e] = lane * E + e;
           aA[e] = M.lds_off + (unsigned)(tri_n(r[e]) * (int)sizeof(T));
           aB[e] = M.lds_off + (unsigned)(r[e] * (int)sizeof(T));
+          // opaque bases: otherwise the compiler hoists the 2 x 32 column
+          // addresses of every inlined product out of the main loop and, at
+          // 256 registers, spills them (215 scratch reloads per iteration)
+          __asm__ volatile("" : "+v"(aA[e]), "+v"(aB[e]), "+v"(r[e]));
         }
         packed_cols<LPC, E, T, 0, false>(aA, aB, r, p, acc);
 #pragma unroll
@@ -280,6 +287,7 @@ __device__ __forceinline__ void momentum_from(const MassDev<T, E, K>& M, const T
         for (int e = 0; e < E; ++e) {
           r[e] = lane * E + e;
           aA[e] = M.chol_off + (unsigned)(tri_n(r[e]) * (int)sizeof(T));
+          __asm__ volatile("" : "+v"(aA[e]), "+v"(r[e]));  // (as in inv_mul: not hoisted)
         }
         packed_cols<LPC, E, T, 0, true>(aA, aA, r, z, acc);
 #pragma unroll
@@ -550,8 +558,11 @@ template <> struct MachEps<double> { static constexpr double v = 2.2204460492503
 
 // find_reasonable_epsilon_with_mass (generic_nuts.rs:1025-1102), identity mass.
 // (not inlined: called once per launch at most, it would otherwise put its
-// leapfrog loops and their registers into the hot tree loop's code)
-template <int LPC, int E, class T, class TG>
+// leapfrog loops and their registers into the hot tree loop's code). One
+// copy per kernel instantiation (TAG = the kernel's MASS): an out-of-line
+// function shared by kernels of different launch bounds is compiled once,
+// and its registers then count against the most demanding caller's budget.
+template <int LPC, int E, class T, class TG, int TAG = 0>
 __device__ __attribute__((noinline)) T find_reasonable_epsilon(const TG& tg, const T (&q0)[E], const T (&p0)[E], int lane, int D) {
   const T half = (T)0.5;
   T eps = (T)1;
@@ -631,7 +642,8 @@ __device__ unsigned long long gm_nuts_prof_buf[NPROF_WAVES * NPROF_SLOTS];
 // SIMD f64 64x4 +4 %, 64x8 +78 %, 64x16 +150 %, f32 64x16 +55 %, but f32
 // 64x4 -6 % and 64x8 -4 %, which therefore keep 2.
 template <class T, int LPC, int E, class TG, int MASS>
-__global__ __launch_bounds__(256, (MASS == 2 || E * (int)sizeof(T) > 32 || (sizeof(T) == 8 && E > 2)) ? 1 : 2)
+__global__ __launch_bounds__(256, MASS == 2 ? GM_DENSE_WAVES : MASS == 3 ? GM_FROZEN_WAVES
+                                  : (E * (int)sizeof(T) > 32 || (sizeof(T) == 8 && E > 2)) ? 1 : 2)
 void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
@@ -729,7 +741,11 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   M.D = D;
   int rn = 0;
   T rmean[E], rm2d[E];
-  if (MASS && a.mass_mode) {
+  if (MASS == 3) {  // every chain dense (the host checked a.mkind)
+    M.minvT = (const T*)a.minv + (long long)c * D * D;
+    M.cholT = (const T*)a.mchol + (long long)c * D * D;
+  }
+  if (MASS && MASS != 3 && a.mass_mode) {
     M.kind_ = a.mkind[c];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -742,6 +758,11 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     if (MASS == 2 && a.mass_mode == 2) {
       M.minvT = (const T*)a.minv + (long long)c * D * D;
       M.cholT = (const T*)a.mchol + (long long)c * D * D;
+    }
+    rn = a.rn[c];
+  }
+  if (MASS >= 2 && a.mass_mode == 2) {
+    {
       if constexpr (LPC == 16 && E == 2) {
         if (a.minv_lds == 2) {
           // the chain's M^-1 into its LDS slot, full and transposed ([j][i]):
@@ -785,7 +806,6 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
         }
       }
     }
-    rn = a.rn[c];
   }
 
   if (a.do_init) {  // init_chain_state (generic_nuts.rs:731-753)
@@ -802,10 +822,10 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     T qc[E], pc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) { qc[e] = q[e]; pc[e] = p0[e]; }
-    if ((ae < (T)0 ? -ae : ae) <= MachEps<T>::v) eps = find_reasonable_epsilon<LPC, E>(tg, qc, pc, lane, D);
+    if ((ae < (T)0 ? -ae : ae) <= MachEps<T>::v) eps = find_reasonable_epsilon<LPC, E, T, decltype(tg), MASS>(tg, qc, pc, lane, D);
     mu = glog((T)10 * eps);
   }
-  if (a.do_refind && a.updated[c]) {  // after a metric update (generic_nuts.rs:905-918)
+  if (MASS != 3 && a.do_refind && a.updated[c]) {  // after a metric update (generic_nuts.rs:905-918)
     T z[E], probe[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -816,7 +836,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     T qc[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) qc[e] = q[e];
-    eps = find_reasonable_epsilon<LPC, E>(tg, qc, probe, lane, D);  // identity-mass leapfrog (:1009-1023)
+    eps = find_reasonable_epsilon<LPC, E, T, decltype(tg), MASS>(tg, qc, probe, lane, D);  // identity-mass leapfrog (:1009-1023)
     mu = glog((T)10 * eps);
     eps_bar = eps;
     h_bar = (T)0;
@@ -839,17 +859,22 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
                              // measured -6 %, profiles/r04/ab_nuts_joint_momentum_refill.log)
   const bool track = a.trk.mean != nullptr;  // run_progress (generic_nuts.rs:688-704)
   ChainTrack<LPC, E> tr;
-  if (track) tr.load(a.trk, c, lane, D);
+  // (the frozen-dense kernel keeps the tracker's vectors in memory between
+  // transitions: its registers are short)
+  if (track) {
+    if constexpr (MASS == 3) tr.p = a.trk.p[c];
+    else tr.load(a.trk, c, lane, D);
+  }
 
   // per-chain loop state
   int s = 0;             // transitions completed in this launch
   bool starting = true;  // the next evaluation starts transition s
-  T p0[E];               // the transition's momentum (starting chains)
+  T p0o[E];              // the transition's momentum (starting chains)
   T qe[E], pe[E], ge[E];  // edge: the trajectory end on side v (being integrated)
   T qf[E], pf[E], gf[E];  // the far end
   // dense metric: M^-1 p and M^-1 g of both ends, carried by linearity
   // (carried_velocity below); the start's M^-1 p0
-  T ve[E], we[E], vf[E], wf[E], v0[E];
+  T ve[E], we[E], vf[E], wf[E], v0o[E];
   int v = 1, j = 0;
   // tree counts fit 32 bits: the depth cap (<= NUTS_MAX_DEPTH_LIMIT = 30) bounds n by 2^30
   int l = 0, n = 1;
@@ -862,8 +887,8 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   T ta = (T)0;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    qe[e] = pe[e] = ge[e] = qf[e] = pf[e] = gf[e] = fq[e] = fp[e] = pr[e] = p0[e] = (T)0;
-    ve[e] = we[e] = vf[e] = wf[e] = v0[e] = (T)0;
+    qe[e] = pe[e] = ge[e] = qf[e] = pf[e] = gf[e] = fq[e] = fp[e] = pr[e] = p0o[e] = (T)0;
+    ve[e] = we[e] = vf[e] = wf[e] = v0o[e] = (T)0;
   }
 
 #ifdef GM_NUTS_PROF
@@ -889,7 +914,9 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   // would also wait out the previous transition's sample stores.
   __builtin_amdgcn_s_waitcnt(0);
   const ExpConsts ek = [] {  // the leaf's f64 exp, constants in VGPRs
-    if constexpr (sizeof(T) == 8) return ExpConsts::pinned();
+    // (not in the frozen-dense kernel: at its 2 waves per SIMD the 20
+    // registers are worth more than the scalar operands they save)
+    if constexpr (sizeof(T) == 8 && MASS != 3) return ExpConsts::pinned();
     else return ExpConsts{};
   }();
   while (true) {
@@ -919,6 +946,21 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     const T h = epsv * (T)0.5;
     // --- the evaluation point: q (a starting transition) or the next leaf
     T x[E], gx[E];
+    // The start's momentum p0 and M^-1 p0 are used in the iteration that
+    // draws them only. The frozen-dense kernel keeps them iteration-local
+    // (zero elsewhere: 8 registers it cannot spare); the others keep the
+    // loop-carried arrays of their measured schedule.
+    T p0l[E], v0l[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) p0l[e] = v0l[e] = (T)0;
+    T (&p0)[E] = [&]() -> T (&)[E] {
+      if constexpr (MASS == 3) return p0l;
+      else return p0o;
+    }();
+    T (&v0)[E] = [&]() -> T (&)[E] {
+      if constexpr (MASS == 3) return v0l;
+      else return v0o;
+    }();
     if (live && starting) {  // momentum (generic_nuts.rs:758-762)
       T z[E];
 #pragma unroll
@@ -948,7 +990,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       if (live && !starting) {  // leapfrog_with_mass (:1396-1418): kick, drift by M^-1 p
 #pragma unroll
         for (int e = 0; e < E; ++e) pe[e] = pe[e] + ge[e] * h;
-        if (MASS == 2 && M.kind() == 2) {
+        if (MASS >= 2 && M.kind() == 2) {
 #pragma unroll
           for (int e = 0; e < E; ++e) vv[e] = ve[e] + we[e] * h;
         } else {
@@ -975,7 +1017,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       T pk[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) pk[e] = starting ? p0[e] : pe[e];
-      if constexpr (MASS == 2) {
+      if constexpr (MASS >= 2) {
         // carried_velocity: one product per evaluation (M^-1 g) instead of
         // two (the drift's M^-1 p and the kinetic energy's); a starting
         // chain's M^-1 p0 only in iterations where some chain of the wave
@@ -1032,7 +1074,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
         qe[e] = q[e]; pe[e] = p0[e]; ge[e] = gx[e];
         qf[e] = q[e]; pf[e] = p0[e]; gf[e] = gx[e];
       }
-      if constexpr (MASS == 2) {
+      if constexpr (MASS >= 2) {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           ve[e] = v0[e]; we[e] = wx[e];
@@ -1052,7 +1094,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     ++nlf;
 #pragma unroll
     for (int e = 0; e < E; ++e) ge[e] = gx[e];
-    if constexpr (MASS == 2) {
+    if constexpr (MASS >= 2) {
 #pragma unroll
       for (int e = 0; e < E; ++e) { ve[e] = vv[e]; we[e] = wx[e]; }
     }
@@ -1140,7 +1182,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       {
         // the trajectory's ends: the edge (qe, pe) on side v and the far end
         // (qf, pf), unordered (no_uturn_ends)
-        if constexpr (MASS == 2) {  // dense: the ends' carried M^-1 p (no product)
+        if constexpr (MASS >= 2) {  // dense: the ends' carried M^-1 p (no product)
           if (s_ok) {
             if (M.kind() == 2) s_ok = no_uturn_ends<LPC, E>(qe, qf, ve, vf, v);
             else s_ok = no_uturn_ends_m<LPC, E>(M, qe, qf, pe, pf, v, lane);
@@ -1164,7 +1206,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
           pf[e] = sw ? a1 : pf[e];
           gf[e] = sw ? a2 : gf[e];
         }
-        if constexpr (MASS == 2) {
+        if constexpr (MASS >= 2) {
 #pragma unroll
           for (int e = 0; e < E; ++e) {
             const T b0 = ve[e], b1 = we[e];
@@ -1194,7 +1236,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       eps_bar = gexp(((T)1 - eta) * glog(eps_bar) + eta * glog(eps));
       // RunningCov::update inside the collection window (:897-903, 108-129)
       const long long lim = a.n_discard > a.eb ? a.n_discard - a.eb : 0;
-      if (MASS && a.mass_mode && m > a.sb && m < lim) {
+      if (MASS && MASS != 3 && a.mass_mode && m > a.sb && m < lim) {
         rn += 1;
         const T ns = (T)rn;
         T d1[E], d2[E];
@@ -1220,7 +1262,11 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     } else {
       eps = eps_bar;
     }
-    if (track) tr.step(q, a.trk.n0 + (unsigned long long)s + 1ull, lane, D);
+    if (track) {
+      if constexpr (MASS == 3) tr.load_vec(a.trk, c, lane, D);
+      tr.step(q, a.trk.n0 + (unsigned long long)s + 1ull, lane, D);
+      if constexpr (MASS == 3) tr.store_vec(a.trk, c, lane, D);
+    }
     record(a.t0 + s + 1);
     ++s;
     starting = true;
@@ -1240,8 +1286,14 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     }
   }
 #endif
-  if (track) tr.store(a.trk, c, lane, D);
-  if (MASS && a.mass_mode) {
+  if (track) {
+    if constexpr (MASS == 3) {
+      if (lane == 0) a.trk.p[c] = tr.p;
+    } else {
+      tr.store(a.trk, c, lane, D);
+    }
+  }
+  if (MASS && MASS != 3 && a.mass_mode) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;

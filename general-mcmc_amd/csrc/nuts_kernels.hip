@@ -395,6 +395,22 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     if (ns.mass_mode == 2) hipMemsetAsync(ns.rm2, 0, (size_t)C * D * D * esz, st);
     hipMemsetAsync(ns.updated, 0, C * sizeof(int), st);
   }
+  // The frozen-dense instantiation (MASS 3) for launches without a window
+  // end or Welford collection when every chain's metric is dense: read the
+  // chains' kinds back once (after the stream's earlier work)
+  bool all_dense = false;
+  bool any_update = false;
+  for (char u : seg_update) any_update = any_update || u;
+  if (ns.mass_mode == 2 && !any_update && tg.kind != GM_TARGET_CUSTOM && lay.lanes == 16 && lay.elems == 2) {
+    std::vector<int> kinds((size_t)C);
+    if (hipMemcpyAsync(kinds.data(), ns.mkind, C * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+      set_error("copy of the NUTS metric kinds failed");
+      return GM_EHIP;
+    }
+    all_dense = C > 0;
+    for (int k : kinds) all_dense = all_dense && k == 2;
+  }
   int pending_refind = 0;
   uint64_t refind_step = 0;
   NutsLdsBudget budget;
@@ -480,6 +496,9 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
       a.eb = ns.m_eb;
       a.do_refind = pending_refind;
       a.refind_step = refind_step;
+      // no Welford collection in the launch: every m >= lim or m <= start_buffer
+      const long long lim = ns.n_discard > ns.m_eb ? ns.n_discard - ns.m_eb : 0;
+      a.dense_frozen = (all_dense && !a.do_refind && (a.m0 + 1 >= lim || a.m0 + nst <= ns.m_sb)) ? 1 : 0;
     }
     if (trk) {
       a.trk = *trk;
@@ -501,6 +520,7 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     ns.plan[2] = (int)a.minv_lds_off;
     ns.plan[3] = a.chol_lds;
     ns.plan[4] = (int)a.chol_lds_off;
+    ns.plan[5] = a.dense_frozen;
     if (e != hipSuccess) {
       set_error(std::string("NUTS launch failed: ") + hipGetErrorString(e));
       return GM_EHIP;

@@ -32,10 +32,13 @@ inline size_t nuts_size_lds(NutsLaunch& a, const NutsLdsBudget& b, unsigned bloc
   const size_t per_level = (size_t)3 * 256 * E * tsz + (size_t)(256 / LPC) * (tsz + 8);
   long long bpc = ((long long)blocks + b.ncu - 1) / b.ncu;
   bpc = bpc < 1 ? 1 : bpc > 4 ? 4 : bpc;
-  // the dense-metric kernel runs one wave per SIMD (its launch bound: 512
+  // the dense-metric kernels run GM_DENSE_WAVES (adaptive: one, 512
   // registers per lane, the metric's products and state without scratch
-  // spills), so one block per CU holds the CU's LDS
-  if (a.mass_mode == 2) bpc = 1;
+  // spills) or GM_FROZEN_WAVES (frozen) waves per SIMD, i.e. blocks per CU
+  if (a.mass_mode == 2) {
+    const long long w = a.dense_frozen ? GM_FROZEN_WAVES : GM_DENSE_WAVES;
+    bpc = bpc < w ? bpc : w;
+  }
   size_t budget = (size_t)(160 * 1024) / (size_t)bpc - 1024;
   if (budget > (size_t)b.lds_max) budget = (size_t)b.lds_max;
   // Dense metric (layout 16 x 2): the block's chains' M^-1 resident in LDS,

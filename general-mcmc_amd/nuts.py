@@ -114,10 +114,10 @@ class NUTS(Sampler):
 
     def launch_plan(self) -> dict:
         """The last launch's on-chip plan (gm_nuts_get_plan)."""
-        p = np.zeros(5, dtype=np.int32)
+        p = np.zeros(6, dtype=np.int32)
         _lib.check(self._lib.gm_nuts_get_plan(self._h, _lib.ptr(p)))
         return {"lds_levels": int(p[0]), "minv_lds": int(p[1]), "minv_off": int(p[2]), "chol_lds": int(p[3]),
-                "chol_off": int(p[4])}
+                "chol_off": int(p[4]), "frozen": int(p[5])}
 
     def step_sizes(self) -> tuple[np.ndarray, np.ndarray]:
         """Per-chain (epsilon, epsilon_bar)."""

@@ -244,7 +244,9 @@ int gm_nuts_set_dense_forms(gm_sampler* s, int32_t minv_lds, int32_t chol_lds);
 
 /* The last NUTS launch's on-chip plan: plan[0] subtree-stack levels in LDS,
  * plan[1] M^-1 form (0 global, 1 packed, 2 full), plan[2] its LDS offset,
- * plan[3] Cholesky factor in LDS (0/1), plan[4] its offset. */
+ * plan[3] Cholesky factor in LDS (0/1), plan[4] its offset, plan[5] 1 when
+ * the launch ran the frozen-dense kernel (every chain's metric dense, no
+ * warm-up window: GM_FROZEN_WAVES waves per SIMD). plan holds 6 values. */
 int gm_nuts_get_plan(gm_sampler* s, int32_t* plan);
 
 int gm_nuts_get_mass(gm_sampler* s, int32_t* mode, int32_t* kind, void* dinv, void* dsqrt, void* minv,
@@ -274,6 +276,11 @@ int gm_sampler_synchronize(gm_sampler* s);
 
 /* Transitions per kernel launch (state stays in registers inside a launch). */
 int gm_sampler_set_steps_per_launch(gm_sampler* s, int64_t steps);
+
+/* HMC leapfrog-loop unroll of the fused kernel: 0 (default) chosen by the
+ * launch's waves per SIMD, or forced to 1, 2 or 4 (tests and measurements;
+ * identical results in every form). No reference counterpart. */
+int gm_sampler_set_unroll(gm_sampler* s, int32_t n);
 
 /* Pre-size the device sample buffer for runs collecting up to n_collect
  * transitions, so that a later gm_run / gm_run_device does no device

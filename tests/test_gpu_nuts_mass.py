@@ -119,6 +119,26 @@ def test_dense_warmup_matrix_core_layout(gm, oracle, minv_lds, chol_lds, D, chai
     assert plan["chol_lds"] <= int(chol_lds) and (plan["chol_lds"] == 0 or plan["minv_lds"] == 1)
 
 
+@pytest.mark.parametrize("D,chains,dtype", [(32, 36, np.float64), (20, 10, np.float64), (32, 36, np.float32)])
+def test_dense_frozen_sampling_bitexact(gm, oracle, D, chains, dtype):
+    """After the warm-up, a run without windows (run(n, 0), the bench's
+    sampling phase) with every chain's metric dense takes the frozen-dense
+    kernel (MASS 3: no identity/diagonal branches, no Welford state, two
+    waves per SIMD at 16 x 2) -- the same bits as the oracle, partial wave
+    included; a later warm-up run goes back to the adaptive kernel."""
+    rng = np.random.default_rng(31)
+    a = rng.standard_normal((D, D))
+    cov = a @ a.T / D + 0.5 * np.eye(D)
+    t = _gauss(gm, cov, rng.standard_normal(D))
+    x0 = gm.init_with_seed(chains, D, 7, np.float64).astype(dtype)
+    s, om = _check_run(gm, oracle, t, x0, dtype, 2, [(1, 60), (25, 0), (6, 20), (9, 0)], start_buffer=4,
+                       end_buffer=4, initial_window=10, layout=(16, 2))
+    assert np.all(om.kind == 2)
+    assert s.launch_plan()["frozen"] == 1
+    s.run(2, 20)
+    assert s.launch_plan()["frozen"] == 0
+
+
 def test_progress_semantics_with_mass(gm, oracle):
     t = _gauss(gm, np.diag([0.25, 2.0, 1.0]))
     x0 = gm.init_with_seed(10, 3, 6, np.float64)

@@ -77,6 +77,26 @@ def test_hmc_samples_bitwise(gm, oracle, dtype, dim, lay):
         s.close()
 
 
+@pytest.mark.parametrize("unroll", [1, 2, 4])
+@pytest.mark.parametrize("L", [7, 8, 1])
+@pytest.mark.parametrize("dim,lay,dtype", [(64, (64, 1), np.float32), (128, (64, 2), np.float32),
+                                           (32, (16, 2), np.float64)])
+def test_hmc_unroll_forms_bitwise(gm, oracle, unroll, L, dim, lay, dtype):
+    """The fused kernel's leapfrog loop unrolled x1, x2 and x4 (chosen by the
+    launch's waves per SIMD; forced here with gm_sampler_set_unroll), odd,
+    even and single leapfrog counts: the oracle's bits in every form."""
+    n_chains, eps = 24, 0.01
+    x0 = start(gm, n_chains, dim, dtype)
+    t = gm.RosenbrockND()
+    s = gm.HMC(t, x0, eps, L, dtype=dtype).set_seed(5)
+    s.set_layout(*lay)
+    s.set_unroll(unroll)
+    out = s.run(3, 2)
+    q, samples, acc = oracle.hmc_run(Target.from_product(t, dim), x0, eps, L, 5, 0, 5, 2, *lay)
+    np.testing.assert_array_equal(out, samples.transpose(1, 0, 2))
+    np.testing.assert_array_equal(s.accept_counts(), acc)
+
+
 @pytest.mark.parametrize("dim,elems", [(33, 1), (50, 1), (64, 1), (65, 2), (100, 2), (128, 2)])
 @pytest.mark.parametrize("n_chains,offset", [(2, 0), (10, 7), (11, 3), (64, 1)])
 def test_hmc_64lane_rosenbrock_bitwise(gm, oracle, dim, elems, n_chains, offset):

@@ -112,6 +112,19 @@ def test_tab_normal_f32_momenta(oracle):
     for w2 in (0, 0x12345678, 0xFFFFFFFF):
         lib.or_tab_normal_pair_f(0xFFFFFFFF, w2, out)
         assert out[0] == 0.0 and out[1] == 0.0
+    # u1 -> 1 (the words random draws almost never reach): ln u1 = -ln2 +
+    # ln c_127 + ln(1 + r) cancels to a few ulps of 0.69, and the radius is
+    # small there. The bound holds in the whole band w1 >= 0xFFFF0000 (every
+    # 7th word, and the last 512 words exhaustively; measured <= 2.1e-8).
+    w1s = list(range(0xFFFF0000, 0xFFFFFE00, 7)) + list(range(0xFFFFFE00, 0xFFFFFFFF))
+    worst = 0.0
+    for w1 in w1s:
+        w2 = (w1 * 2654435761) & 0xFFFFFFFF
+        lib.or_tab_normal_pair_f(w1, w2, out)
+        u1, u2 = ((w1 >> 8) + 1) * 2.0 ** -24, (w2 >> 8) * 2.0 ** -24
+        r = math.sqrt(-2.0 * math.log(u1))
+        worst = max(worst, abs(out[0] - r * math.cos(2 * math.pi * u2)), abs(out[1] - r * math.sin(2 * math.pi * u2)))
+    assert worst < 1.5e-6, worst
 
 
 def test_tab_normal_u1_one_is_zero(oracle):
