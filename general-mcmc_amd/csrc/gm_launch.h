@@ -92,6 +92,7 @@ struct NutsLaunch {
   void* dsq = nullptr;       // [C][D]
   void* minv = nullptr;      // [C][D][D]
   void* mchol = nullptr;     // [C][D][D]
+  void* mchol_rm = nullptr;  // [C][D][D] + D slack: L row-major (mchol is the per-chain transpose)
   int* rn = nullptr;         // [C] RunningCov::n
   void* rmean = nullptr;     // [C][D]
   void* rm2d = nullptr;      // [C][D]

@@ -35,6 +35,7 @@ template <class T, int E, int K = 2> struct MassDev {
   int minv_lds = 0;          // M^-1 resident in LDS: 1 packed (minv_packed_lds), 2 full; the chain's slot at lds_off
   unsigned lds_off = 0;
   const T* cholT = nullptr;  // its Cholesky factor L, transposed: cholT[j][i] = L_ij
+  const T* cholR = nullptr;  // L row-major (cholR[i][j] = L_ij; the 16 x 2 start's rows)
   int chol_lds = 0;          // L resident in LDS, rows packed: the chain's slot at chol_off
   unsigned chol_off = 0;
   int D = 0;
@@ -89,13 +90,19 @@ __device__ __forceinline__ void row_bcasts(const T (&p)[E], T (&pj)[NB]) {
 // rows/columns of the triangle are exactly +0, and adding +0 leaves an
 // accumulator that starts at +0 unchanged (it can never become -0: x + y
 // rounds to -0 only when both are -0), so the padded columns change no bit.
+// (PB columns per batch: 8 at one wave per SIMD, 4 in the frozen-dense
+// kernel at two, where 8 cost 12 more spilled registers: measured 9.19e8 vs
+// 9.58e8 leapfrogs/s at cfg3_dense, profiles/r05/ab_dense_batches.log)
 #ifndef GM_PACKED_BATCH
 #define GM_PACKED_BATCH 8
 #endif
-template <int LPC, int E, class T, int J, bool CHOL>
+#ifndef GM_FROZEN_PACKED_BATCH
+#define GM_FROZEN_PACKED_BATCH 4
+#endif
+template <int LPC, int E, class T, int J, bool CHOL, int PB = GM_PACKED_BATCH>
 __device__ __forceinline__ void packed_cols(const unsigned (&aA)[E], const unsigned (&aB)[E], const int (&r)[E],
                                             const T (&p)[E], T (&acc)[E]) {
-  constexpr int NB = GM_PACKED_BATCH < LPC * E - J ? GM_PACKED_BATCH : LPC * E - J;
+  constexpr int NB = PB < LPC * E - J ? PB : LPC * E - J;
   if constexpr (NB > 0) {
     T m[NB][E], pj[NB];
 #pragma unroll
@@ -125,7 +132,7 @@ __device__ __forceinline__ void packed_cols(const unsigned (&aA)[E], const unsig
         else acc[e] = gfma(mm, pj[u], acc[e]);  // M^-1 p: the engine's fma chain (oracle inv_mul)
       }
     }
-    packed_cols<LPC, E, T, J + NB, CHOL>(aA, aB, r, p, acc);
+    packed_cols<LPC, E, T, J + NB, CHOL, PB>(aA, aB, r, p, acc);
   }
 }
 
@@ -154,11 +161,15 @@ __device__ __forceinline__ void full_cols(unsigned base, const T (&p)[E], T (&ac
   }
 }
 
-// Columns [J, J + NB) of p = L z from the global factor (cholT[j][i] = L_ij,
-// row stride D <= 32) when it is not resident in LDS (the full-M^-1 budget):
-// the batch's loads, clamped to valid addresses, and row broadcasts first,
-// then the sums in ascending j. Terms with j > i (L_ij = 0 there), padded
-// rows (i >= D) and padded columns (z_j = +0) add +-0 to the +0-started sum:
+// Columns [J, J + NB) of p = L z from the global factor when it is not
+// resident in LDS: each lane reads its own rows of the row-major L (pb[e] =
+// row r, clamped to a valid row; column j at the immediate offset 8j, so no
+// address arithmetic and no hoisted column offsets -- the transposed form's
+// j*D offsets were kept in spilled scalars; the buffer has D elements of
+// slack past the last row for the padded columns j >= D of a D < 32 chain).
+// The batch's loads and row broadcasts first, then the sums in ascending j.
+// Terms with j > i (L_ij = 0 there, and every padded column), padded rows
+// (i >= D) and padded coordinates (z_j = +0) add +-0 to the +0-started sum:
 // no bit changes, as in packed_cols.
 #ifndef GM_CHOL_BATCH
 #define GM_CHOL_BATCH 8
@@ -172,9 +183,8 @@ __device__ __forceinline__ void chol_global_cols(const T* const (&pb)[E], int D,
     T m[NB][E], zj[NB];
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
-      const int j = (J + u < D) ? J + u : D - 1;
 #pragma unroll
-      for (int e = 0; e < E; ++e) m[u][e] = pb[e][j * D];
+      for (int e = 0; e < E; ++e) m[u][e] = pb[e][J + u];
     }
     row_bcasts<E, T, J, 0, NB>(z, zj);
     __builtin_amdgcn_sched_barrier(0);
@@ -208,7 +218,9 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E, K>& M, const T (&p)[
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
     if constexpr (LPC == 16 && E == 2) {
-      if (M.minv_lds == 2) {
+      // (the frozen-dense kernel's plan is the packed triangle or global
+      // memory: its 2 blocks per CU leave no room for the full form)
+      if (K != 3 && M.minv_lds == 2) {
         // (software-pipelining the batches, batch J+1's reads and broadcasts
         // issued before batch J's sums, measured -1 % / -5 % at 4 / 8
         // columns per batch, profiles/r04/ab_dense_pipe.log: not kept)
@@ -230,7 +242,7 @@ __device__ __forceinline__ void inv_mul(const MassDev<T, E, K>& M, const T (&p)[
           // 256 registers, spills them (215 scratch reloads per iteration)
           __asm__ volatile("" : "+v"(aA[e]), "+v"(aB[e]), "+v"(r[e]));
         }
-        packed_cols<LPC, E, T, 0, false>(aA, aB, r, p, acc);
+        packed_cols<LPC, E, T, 0, false, K == 3 ? GM_FROZEN_PACKED_BATCH : GM_PACKED_BATCH>(aA, aB, r, p, acc);
 #pragma unroll
         for (int e = 0; e < E; ++e) v[e] = acc[e];
         return;
@@ -280,7 +292,7 @@ __device__ __forceinline__ void momentum_from(const MassDev<T, E, K>& M, const T
 #pragma unroll
     for (int e = 0; e < E; ++e) acc[e] = (T)0;
     if constexpr (LPC == 16 && E == 2) {
-      if (M.chol_lds) {
+      if (K != 3 && M.chol_lds) {  // (never in the frozen-dense plan)
         unsigned aA[E];
         int r[E];
 #pragma unroll
@@ -302,8 +314,9 @@ __device__ __forceinline__ void momentum_from(const MassDev<T, E, K>& M, const T
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           r[e] = lane * E + e;
-          pb[e] = M.cholT + (r[e] < M.D ? r[e] : M.D - 1);
-          __asm__ volatile("" : "+v"(pb[e]));
+          pb[e] = M.cholR + (long long)(r[e] < M.D ? r[e] : M.D - 1) * M.D;
+          // opaque: else the 2 x 32 masks (j > r) are hoisted and spilled
+          __asm__ volatile("" : "+v"(pb[e]), "+v"(r[e]));
         }
         chol_global_cols<LPC, E, T, 0>(pb, M.D, r, z, acc);
 #pragma unroll
@@ -744,6 +757,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   if (MASS == 3) {  // every chain dense (the host checked a.mkind)
     M.minvT = (const T*)a.minv + (long long)c * D * D;
     M.cholT = (const T*)a.mchol + (long long)c * D * D;
+    M.cholR = (const T*)a.mchol_rm + (long long)c * D * D;
   }
   if (MASS && MASS != 3 && a.mass_mode) {
     M.kind_ = a.mkind[c];
@@ -758,6 +772,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     if (MASS == 2 && a.mass_mode == 2) {
       M.minvT = (const T*)a.minv + (long long)c * D * D;
       M.cholT = (const T*)a.mchol + (long long)c * D * D;
+      M.cholR = (const T*)a.mchol_rm + (long long)c * D * D;
     }
     rn = a.rn[c];
   }

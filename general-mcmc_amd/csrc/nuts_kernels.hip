@@ -253,7 +253,9 @@ int nuts_set_mass(NutsState* ns, gm_dtype dt, long long C, int D, int mode, long
   if (e == hipSuccess) e = hipMalloc((void**)&ns->updated, C * sizeof(int));
   if (mode == 2) {
     if (e == hipSuccess) e = hipMalloc(&ns->minv, cdd);
-    if (e == hipSuccess) e = hipMalloc(&ns->mchol, cdd);
+    // (+ D elements: the 16 x 2 start's row reads run past a chain's last row
+    // into the padded columns of a D < 32 metric; nuts_device.h chol_global_cols)
+    if (e == hipSuccess) e = hipMalloc(&ns->mchol, cdd + (size_t)D * esz);
     if (e == hipSuccess) e = hipMalloc(&ns->rm2, cdd);
     if (e == hipSuccess) e = hipMalloc(&ns->mscratch, 4 * cdd);
   }
@@ -267,7 +269,7 @@ int nuts_set_mass(NutsState* ns, gm_dtype dt, long long C, int D, int mode, long
   hipMemset(ns->dsq, 0, cd);
   if (mode == 2) {
     hipMemset(ns->minv, 0, cdd);
-    hipMemset(ns->mchol, 0, cdd);
+    hipMemset(ns->mchol, 0, cdd + (size_t)D * esz);
   }
   ns->mass_mode = mode;
   ns->m_sb = start_buffer;
@@ -467,6 +469,7 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
       a.dsq = ns.dsq;
       a.minv = ns.minv;
       a.mchol = ns.mchol;
+      a.mchol_rm = ns.mchol;
       if (ns.mass_mode == 2) {  // the transposes, in the update kernel's scratch (free between its launches)
         const size_t esz = dt == GM_F32 ? 4 : 8, cdd = (size_t)C * D * D * esz;
         void* mT = ns.mscratch;

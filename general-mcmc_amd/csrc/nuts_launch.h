@@ -51,10 +51,14 @@ inline size_t nuts_size_lds(NutsLaunch& a, const NutsLdsBudget& b, unsigned bloc
   a.chol_lds = 0;
   a.chol_lds_off = 0;
   if (a.mass_mode == 2 && b.minv_lds && LPC == 16 && E == 2 && a.D <= LPC * E) {
+    // the frozen-dense kernel (nuts_device.h MASS 3) takes the packed M^-1
+    // only (no full form, no L in LDS)
+    const int want = a.dense_frozen ? 1 : b.minv_lds;
+    const int want_chol = a.dense_frozen ? 0 : b.chol_lds;
     const size_t dp = (size_t)LPC * E;
     const size_t mb = (size_t)(256 / LPC) * (dp * (dp + 1) / 2) * tsz;
     const size_t mf = (size_t)(256 / LPC) * dp * dp * tsz;
-    if (b.minv_lds != 1 && tgl + mf <= budget) {  // the full matrices (no address arithmetic)
+    if (want != 1 && tgl + mf <= budget) {  // the full matrices (no address arithmetic)
       a.minv_lds = 2;
       a.minv_lds_off = (unsigned)tgl;
       tgl += (mf + 15) / 16 * 16;
@@ -62,7 +66,7 @@ inline size_t nuts_size_lds(NutsLaunch& a, const NutsLdsBudget& b, unsigned bloc
       a.minv_lds = 1;
       a.minv_lds_off = (unsigned)tgl;
       tgl += (mb + 15) / 16 * 16;
-      if (b.chol_lds && tgl + mb <= budget) {
+      if (want_chol && tgl + mb <= budget) {
         a.chol_lds = 1;
         a.chol_lds_off = (unsigned)tgl;
         tgl += (mb + 15) / 16 * 16;
