@@ -931,7 +931,10 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   const ExpConsts ek = [] {  // the leaf's f64 exp, constants in VGPRs
     // (not in the frozen-dense kernel: at its 2 waves per SIMD the 20
     // registers are worth more than the scalar operands they save)
-    if constexpr (sizeof(T) == 8 && MASS != 3) return ExpConsts::pinned();
+#ifndef GM_FROZEN_PIN_EXP
+#define GM_FROZEN_PIN_EXP 0
+#endif
+    if constexpr (sizeof(T) == 8 && (MASS != 3 || GM_FROZEN_PIN_EXP)) return ExpConsts::pinned();
     else return ExpConsts{};
   }();
   while (true) {
