@@ -80,7 +80,36 @@ __device__ __forceinline__ double lane_k(double v, int k) {
   return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
+// A chain of LPC > 64 lanes is the whole workgroup (the wide NUTS layouts,
+// one chain per block of LPC/64 waves): its sum is each wave's 64-lane total
+// (the group_sum<64> order) added over the waves left to right, through LDS
+// (the oracle's order for lanes > 64, as block_sum). Every wave of the block
+// reaches it together: the chain's control flow is uniform over the block.
+template <int LPC, int N, class T> __device__ __forceinline__ void block_totals(T (&v)[N]) {
+  constexpr int W = LPC / 64;
+  __shared__ T red[N][W];
+  const int w = (int)(threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) red[k][w] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    T s = red[k][0];
+#pragma unroll
+    for (int u = 1; u < W; ++u) s = s + red[k][u];
+    v[k] = s;
+  }
+  __syncthreads();  // red is reused by the next sum
+}
+
 template <int LPC, class T> __device__ __forceinline__ T group_sum(T v) {
+  if constexpr (LPC > 64) {
+    T t[1] = {group_sum<64>(v)};
+    block_totals<LPC, 1>(t);
+    return t[0];
+  }
   if constexpr (LPC >= 2) v = v + dpp<DPP_QUAD_XOR1>(v);
   if constexpr (LPC >= 4) v = v + dpp<DPP_QUAD_XOR2>(v);
   if constexpr (LPC >= 8) v = v + dpp<DPP_ROW_HALF_MIRROR>(v);
@@ -123,6 +152,7 @@ template <int LPC, int N, class T> __device__ __forceinline__ void group_sum_n(T
   GM_STAGE(LPC >= 64, lane63(v[k]))
 #undef GM_STAGE
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (LPC > 64) block_totals<LPC, N>(v);
 }
 // lane l receives lane l+1's value. Wave-wide DPP shift: at a group's last
 // lane the value comes from the next group (or 0); callers mask it, since a
@@ -244,8 +274,8 @@ template <class T, int E> struct RosenbrockLane {
   template <int LPC, int E_, bool LOGP>
   __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int) const {
     static_assert(E_ == E, "layout mismatch");
-    if constexpr (LPC == 64) {
-      const T part = eval64<LOGP>(x, g);
+    if constexpr (LPC >= 64) {
+      const T part = LPC == 64 ? eval64<LOGP>(x, g) : eval_cross<LPC, LOGP>(x, g);
       if (LOGP) return -group_sum<LPC>(part);
       return (T)0;
     }
@@ -287,6 +317,8 @@ template <class T, int E> struct RosenbrockLane {
     static_assert(E_ == E, "layout mismatch");
     if constexpr (LPC == 64) {
       return eval64<true>(x, g);
+    } else if constexpr (LPC > 64) {
+      return eval_cross<LPC, true>(x, g);
     } else {
       T t[E];
       const T nx = from_next<LPC>(x[0]);
@@ -312,9 +344,43 @@ template <class T, int E> struct RosenbrockLane {
     }
   }
   __device__ __forceinline__ T finish(T total) const { return -total; }
+  // The 64-lane form for a chain of LPC > 64 lanes, i.e. the whole
+  // workgroup (the wide NUTS layouts): the wave-boundary neighbours x_{i+1}
+  // and (x_{i-1})^2 come from LDS instead of reading 0, so the operands, and
+  // the bits, are those of a single group holding the whole chain. Every
+  // wave of the block evaluates together (the chain's control flow).
+  template <int LPC, bool LOGP>
+  __device__ __forceinline__ T eval_cross(const T (&x)[E], T (&g)[E]) const {
+    constexpr int W = LPC / 64;
+    __shared__ T xb[2][W];  // each wave's lane-0 x[0] and lane-63 x[E-1]^2
+    const int w = (int)(threadIdx.x >> 6), ln = (int)(threadIdx.x & 63);
+    T xx[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) xx[e] = x[e] * x[e];
+    if (ln == 0) xb[0][w] = x[0];
+    if (ln == 63) xb[1][w] = xx[E - 1];
+    __syncthreads();
+    const T bnx = (w + 1 < W) ? xb[0][w + 1 < W ? w + 1 : w] : (T)0;  // wave-uniform reads
+    const T bpxx = (w > 0) ? xb[1][w > 0 ? w - 1 : 0] : (T)0;
+    __syncthreads();  // xb is rewritten by the next evaluation
+    T nx = from_next<64>(x[0]);
+    T pxx = from_prev<64>(xx[E - 1]);
+    nx = (ln == 63) ? bnx : nx;
+    pxx = (ln == 0) ? bpxx : pxx;
+    return eval64_core<LOGP>(x, g, xx, nx, pxx);
+  }
   template <bool LOGP>
   __device__ __forceinline__ T eval64(const T (&x)[E], T (&g)[E]) const {
     constexpr int LPC = 64;
+    T xx[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) xx[e] = x[e] * x[e];
+    const T nx = from_next<LPC>(x[0]);
+    const T pxx = from_prev<LPC>(xx[E - 1]);
+    return eval64_core<LOGP>(x, g, xx, nx, pxx);
+  }
+  template <bool LOGP>
+  __device__ __forceinline__ T eval64_core(const T (&x)[E], T (&g)[E], const T (&xx)[E], T nx, T pxx) const {
     {
       // One chain per wave: the lane shifts read 0 beyond the wave and the
       // padding coordinates are 0, so a boundary lane can only see finite
@@ -323,11 +389,7 @@ template <class T, int E> struct RosenbrockLane {
       // absent (the engine's canonical form for 64-lane groups; the oracle
       // mirrors it), and (x_{i-1})^2 is shifted in from the lane that
       // computed it, so t_{i-1} is one DPP-fed subtract.
-      T xx[E], t[E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) xx[e] = x[e] * x[e];
-      const T nx = from_next<LPC>(x[0]);
-      const T pxx = from_prev<LPC>(xx[E - 1]);
+      T t[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const T xn = (e + 1 < E) ? x[(e + 1 < E) ? e + 1 : e] : nx;

@@ -35,6 +35,8 @@ bool wide_layout_supported(int lanes, int elems, gm_dtype dt);
 // largest dim of the wide path (f32; f64 is half of it)
 constexpr int GM_WIDE_MAX_DIM = 16384;
 Layout default_layout(int D, gm_dtype dt, int kind);
+Layout nuts_wide_default(int D, gm_dtype dt);
+bool nuts_wide_layout_supported(int lanes, int elems);  // nuts_wide.hip
 
 // Events a launcher records around its kernel (either may be null).
 struct LaunchEvents {

@@ -130,5 +130,9 @@ struct NutsLaunch {
 #ifndef GM_FROZEN_WAVES
 #define GM_FROZEN_WAVES 2
 #endif
+// waves per SIMD of the wide NUTS layouts (one chain per workgroup of
+// lanes/64 waves, nuts_wide.hip): 2 up to 16 bytes of state per lane and
+// vector (f64 x 2, f32 x 4), else 1 (f64 x 4 spills 58-140 registers at 2)
+__host__ __device__ constexpr int nuts_wide_waves(int esz, int E) { return esz * E <= 16 ? 2 : 1; }
 
 }  // namespace gm

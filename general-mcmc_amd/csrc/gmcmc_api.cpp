@@ -53,6 +53,21 @@ static int next_pow2(int v) {
   return p;
 }
 
+// NUTS above 256 dimensions (Rosenbrock, isotropic Gaussian): a chain over
+// a workgroup of 2-8 waves (nuts_wide.hip), whose per-lane state fits the
+// registers; the one-wave layouts 64 x 8 / 64 x 16 spilled (f64) there.
+Layout nuts_wide_default(int D, gm_dtype dt) {
+  Layout l;
+  if (dt == GM_F32) {
+    l.lanes = D <= 512 ? 128 : 256;
+    l.elems = 4;
+  } else {
+    l.lanes = D <= 512 ? 256 : 512;
+    l.elems = 2;
+  }
+  return l;
+}
+
 Layout default_layout(int D, gm_dtype dt, int kind) {
   (void)dt;
   Layout l;
@@ -547,6 +562,9 @@ static int create_common(int kind, const gm_target* target, gm_dtype dtype, int6
     // isotropic one)
     s->lay.lanes = next_pow2((int)dim) / 2;
     s->lay.elems = 2;
+  } else if (kind == K_NUTS && dim > 256 && dim <= 1024 &&
+             (target->kind == GM_TARGET_ROSENBROCK || target->kind == GM_TARGET_ISO_GAUSS)) {
+    s->lay = nuts_wide_default((int)dim, dtype);
   }
   hipError_t e = hipGetDevice(&s->device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
@@ -623,9 +641,16 @@ int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems) {
          "CUSTOM targets run one chain per lane (layout 1 x dim)");
   if (s->tg.kind == GM_TARGET_CUSTOM) return GM_OK;
   const bool wide = lanes > 64;
-  GM_REQ(wide ? wide_layout_supported(lanes, elems, s->dt) : layout_supported(lanes, elems),
-         "layout (lanes, elems) is not compiled in");
-  GM_REQ(!wide || s->kind == K_HMC, "wide layouts (lanes > 64) are for the HMC sampler");
+  if (wide && s->kind == K_NUTS) {  // one chain per workgroup (nuts_wide.hip)
+    GM_REQ(nuts_wide_layout_supported(lanes, elems), "wide NUTS layout (lanes, elems) is not compiled in");
+    GM_REQ(s->tg.kind == GM_TARGET_ROSENBROCK || s->tg.kind == GM_TARGET_ISO_GAUSS,
+           "wide NUTS layouts take the Rosenbrock and isotropic Gaussian targets");
+    GM_REQ(s->nuts.mass_mode != 2, "wide NUTS layouts take the identity or diagonal metric");
+  } else {
+    GM_REQ(wide ? wide_layout_supported(lanes, elems, s->dt) : layout_supported(lanes, elems),
+           "layout (lanes, elems) is not compiled in");
+    GM_REQ(!wide || s->kind == K_HMC, "wide layouts (lanes > 64) are for the HMC and NUTS samplers");
+  }
   GM_REQ((long long)lanes * elems >= s->D, "lanes*elems must cover dim");
   GM_REQ((long long)lanes * elems < 2LL * s->D || lanes == 1 ||
              ((long long)(lanes / 2) * elems < s->D),
@@ -1174,6 +1199,8 @@ int gm_nuts_set_mass_adaptation(gm_sampler* s, int32_t mode, int64_t start_buffe
   GM_HIP(hipStreamSynchronize(s->stream));
   // dense only up to dense_max_dim, else diagonal (generic_nuts.rs:613-620)
   if (mode == 2 && s->D > dense_max_dim) mode = 1;
+  // a dense metric's products broadcast within one wave: off the wide layouts
+  if (mode == 2 && layout_is_wide(s->lay)) s->lay = default_layout(s->D, s->dt, s->tg.kind);
   return nuts_set_mass(&s->nuts, s->dt, s->C, s->D, mode, start_buffer, end_buffer, initial_window,
                        regularize, jitter);
 }

@@ -654,9 +654,18 @@ __device__ unsigned long long gm_nuts_prof_buf[NPROF_WAVES * NPROF_SLOTS];
 // (tools/probe_nuts_highdim.py, profiles/r04/nuts_highdim.jsonl): 1 wave per
 // SIMD f64 64x4 +4 %, 64x8 +78 %, 64x16 +150 %, f32 64x16 +55 %, but f32
 // 64x4 -6 % and 64x8 -4 %, which therefore keep 2.
+//
+// Wide chains (LPC > 64; D > 256, identity or diagonal metric, targets with
+// a cross-wave evaluation): one chain per workgroup of LPC/64 waves, every
+// per-chain sum a block reduction (group_sum), so that the chain's state
+// fits the registers without spills (64 x 8 / 64 x 16 f64 spilled 77-1268
+// registers, profiles/r04/nuts_resources.txt); nuts_wide_waves (gm_launch.h)
+// waves per SIMD for them.
 template <class T, int LPC, int E, class TG, int MASS>
-__global__ __launch_bounds__(256, MASS == 2 ? GM_DENSE_WAVES : MASS == 3 ? GM_FROZEN_WAVES
-                                  : (E * (int)sizeof(T) > 32 || (sizeof(T) == 8 && E > 2)) ? 1 : 2)
+__global__ __launch_bounds__(LPC > 256 ? LPC : 256,
+                             MASS == 2 ? GM_DENSE_WAVES : MASS == 3 ? GM_FROZEN_WAVES
+                             : LPC > 64 ? nuts_wide_waves((int)sizeof(T), E)
+                             : (E * (int)sizeof(T) > 32 || (sizeof(T) == 8 && E > 2)) ? 1 : 2)
 void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
@@ -674,7 +683,8 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   // same value); a lane reads back only what it or its group wrote, so no
   // synchronisation. Deeper levels: HBM, vectors [k][field][chain][coord],
   // scalars [k][chain].
-  constexpr int NT = 256;  // threads per block (launch_nuts)
+  // threads per block (nuts_part.inc): 256, or one chain's LPC > 64
+  constexpr int NT = LPC > 64 ? LPC : 256;
   constexpr int CPB = NT / LPC;
   const int KL = a.lds_levels;
   T* __restrict__ lvec = (T*)(gm_dyn_lds + a.lds_stack_off);

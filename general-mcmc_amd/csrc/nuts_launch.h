@@ -29,9 +29,14 @@ struct NutsLdsBudget {
 inline size_t nuts_size_lds(NutsLaunch& a, const NutsLdsBudget& b, unsigned blocks, size_t tgl, int LPC, int E,
                             size_t tsz) {
   tgl = (tgl + 15) / 16 * 16;
-  const size_t per_level = (size_t)3 * 256 * E * tsz + (size_t)(256 / LPC) * (tsz + 8);
+  const int NT = LPC > 64 ? LPC : 256;  // threads per block (one chain per block when wide)
+  const size_t per_level = (size_t)3 * NT * E * tsz + (size_t)(NT / LPC) * (tsz + 8);
   long long bpc = ((long long)blocks + b.ncu - 1) / b.ncu;
   bpc = bpc < 1 ? 1 : bpc > 4 ? 4 : bpc;
+  if (LPC > 64) {  // the wide kernels' resident blocks per CU (their launch bound)
+    const long long rb = (long long)nuts_wide_waves((int)tsz, E) * 4 / (NT / 64);
+    bpc = bpc < rb ? bpc : (rb < 1 ? 1 : rb);
+  }
   // the dense-metric kernels run GM_DENSE_WAVES (adaptive: one, 512
   // registers per lane, the metric's products and state without scratch
   // spills) or GM_FROZEN_WAVES (frozen) waves per SIMD, i.e. blocks per CU
@@ -95,13 +100,17 @@ hipError_t nuts_launch_part4(gm_dtype dt, const TargetDev& tg, const Layout& lay
                              const NutsLdsBudget& b, bool* found);
 hipError_t nuts_launch_part5(gm_dtype dt, const TargetDev& tg, const Layout& lay, NutsLaunch& a, hipStream_t st,
                              const NutsLdsBudget& b, bool* found);
+// the wide layouts (lanes > 64, nuts_wide.hip)
+hipError_t nuts_launch_wide(gm_dtype dt, const TargetDev& tg, const Layout& lay, NutsLaunch& a, hipStream_t st,
+                            const NutsLdsBudget& b, bool* found);
+bool nuts_wide_layout_supported(int lanes, int elems);
 
 inline hipError_t nuts_launch_layout(gm_dtype dt, const TargetDev& tg, const Layout& lay, NutsLaunch& a,
                                      hipStream_t st, const NutsLdsBudget& b) {
   using Fn = hipError_t (*)(gm_dtype, const TargetDev&, const Layout&, NutsLaunch&, hipStream_t,
                             const NutsLdsBudget&, bool*);
-  static const Fn parts[] = {nuts_launch_part0, nuts_launch_part1, nuts_launch_part2,
-                             nuts_launch_part3, nuts_launch_part4, nuts_launch_part5};
+  static const Fn parts[] = {nuts_launch_part0, nuts_launch_part1, nuts_launch_part2, nuts_launch_part3,
+                             nuts_launch_part4, nuts_launch_part5, nuts_launch_wide};
   for (Fn f : parts) {
     bool found = false;
     const hipError_t e = f(dt, tg, lay, a, st, b, &found);

@@ -1,8 +1,9 @@
-"""NUTS throughput at high dimension on the default layouts (64 lanes x E,
-E = 4 / 8 / 16): the launch-bound A/B of ADVICE r03 (2 vs 1 waves per SIMD
-for E >= 4). One JSON line per (dtype, dim):
+"""NUTS throughput at high dimension on the default layouts (round 5: the
+wide layouts above 256 dimensions, a chain per workgroup; 64 lanes x 4 at
+256). One JSON line per (dtype, dim[, layout]):
 
     GMCMC_LIB=abtest/X/libgmcmc.so python tools/probe_nuts_highdim.py
+    PROBE_CASES="f64:1024:256x4,f64:512:128x4" python tools/probe_nuts_highdim.py   # explicit layouts
 """
 import json
 import os
@@ -18,10 +19,18 @@ import general_mcmc_amd as gm  # noqa: E402
 
 def main():
     chains = int(os.environ.get("PROBE_CHAINS", "2048"))
-    for dt in (np.float64, np.float32):
-        for D in (256, 512, 1024):
+    cases = [(dt, D, None) for dt in (np.float64, np.float32) for D in (256, 512, 1024)]
+    if os.environ.get("PROBE_CASES"):
+        cases = []
+        for c in os.environ["PROBE_CASES"].split(","):
+            d, D, lay = c.split(":")
+            cases.append((np.float64 if d == "f64" else np.float32, int(D), tuple(int(v) for v in lay.split("x"))))
+    for dt, D, lay in cases:
+        if True:
             s = gm.NUTS(gm.IsotropicGaussian(1.0), gm.init_det(chains, D).astype(dt), 0.8, dtype=dt,
                         max_depth=8).set_seed(3)
+            if lay:
+                s.set_layout(*lay)
             s.run_positions(1, 30)  # step-size warm-up, untimed
             s.reserve(30)
             lib = gm._lib.load()
