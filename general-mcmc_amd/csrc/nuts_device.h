@@ -693,9 +693,38 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   int* __restrict__ lnna = lnn + KL * CPB;
   const int tix = threadIdx.x;
   const int cib = tix / LPC;  // chain in block
+  // Level 0 of the stack in registers (GM_L0REG): level 0 is half of all
+  // stack traffic -- an even leaf stores itself there and the next leaf
+  // merges with it one iteration later -- and an LDS (or, in the frozen-dense
+  // kernel, whose packed M^-1 fills the LDS, an HBM) round trip on the
+  // merge's critical path. A level-0 entry is a single leaf: its proposal is
+  // its first q, so q and p are kept (8 registers at 16 x 2 f64) and field 2
+  // reads field 0. Measured: cfg3 3.12e9 -> 3.31e9, cfg3_dense 9.75e8 ->
+  // 1.04e9 leapfrogs/s (profiles/r05/ab_*_l0_registers.log).
+#ifndef GM_L0REG
+#define GM_L0REG 1
+#endif
+  // (not on the wide layouts: 512 x 2 Rosenbrock would spill 16 registers,
+  // and their one-chain blocks keep level 0 in LDS)
+  constexpr bool L0REG = GM_L0REG && LPC <= 64;
+  T l0q[E], l0p[E], l0a = (T)0;
+  int l0n = 0, l0na = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) l0q[e] = l0p[e] = (T)0;
+  // (level 1 in registers as well, 12 more: 60 spilled registers and -5 %,
+  // profiles/r05/ab_dense_l1_registers.log; not kept)
   auto stack_store = [&](int k, const T (&f0)[E], const T (&f1)[E], const T (&f2)[E], T al, int nn,
                          int nna) __attribute__((always_inline)) {
-    if (k < KL) {
+    if (L0REG && k == 0) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        l0q[e] = f0[e];
+        l0p[e] = f1[e];
+      }
+      l0a = al;
+      l0n = nn;
+      l0na = nna;
+    } else if (k < KL) {
       T* v = lvec + (long long)k * 3 * NT * E + tix * E;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -724,7 +753,10 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   };
   // field f (0 first q, 1 first p, 2 proposal) of level k
   auto stack_vec = [&](int k, int f, T (&out)[E]) __attribute__((always_inline)) {
-    if (k < KL) {
+    if (L0REG && k == 0) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) out[e] = f == 1 ? l0p[e] : l0q[e];
+    } else if (k < KL) {
       const T* v = lvec + ((long long)k * 3 + f) * NT * E + tix * E;
 #pragma unroll
       for (int e = 0; e < E; ++e) out[e] = v[e];
@@ -738,7 +770,11 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     }
   };
   auto stack_scalars = [&](int k, T& al, int& nn, int& nna) __attribute__((always_inline)) {
-    if (k < KL) {
+    if (L0REG && k == 0) {
+      al = l0a;
+      nn = l0n;
+      nna = l0na;
+    } else if (k < KL) {
       al = lalpha[k * CPB + cib];
       nn = lnn[k * CPB + cib];
       nna = lnna[k * CPB + cib];
