@@ -711,8 +711,9 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   int l0n = 0, l0na = 0;
 #pragma unroll
   for (int e = 0; e < E; ++e) l0q[e] = l0p[e] = (T)0;
-  // (level 1 in registers as well, 12 more: 60 spilled registers and -5 %,
-  // profiles/r05/ab_dense_l1_registers.log; not kept)
+  // (level 1 in registers as well, 12 more: the frozen-dense kernel spilled
+  // 60 registers and ran 5 % slower, cfg3's reached 256 and ran 13 % slower;
+  // profiles/r05/ab_dense_l1_registers.log, ab_cfg3_l1_registers.log)
   auto stack_store = [&](int k, const T (&f0)[E], const T (&f1)[E], const T (&f2)[E], T al, int nn,
                          int nna) __attribute__((always_inline)) {
     if (L0REG && k == 0) {
