@@ -119,6 +119,10 @@ struct NutsLaunch {
   // frozen-dense instantiation (nuts_device.h MASS 3, GM_FROZEN_WAVES waves
   // per SIMD) instead of the general adaptive one
   int dense_frozen = 0;
+  // the launch's transition momenta as standard normals [n_steps][C][D]
+  // (nuts_momenta_kernel: the same Philox/Box-Muller values the kernel would
+  // draw), or null: drawn in the kernel
+  const void* zmom = nullptr;
 };
 
 // waves per SIMD of the NUTS dense-metric instantiations (their launch

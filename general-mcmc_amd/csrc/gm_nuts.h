@@ -45,6 +45,12 @@ struct NutsState {
   void* rm2 = nullptr;        // [C][D][D]
   int* updated = nullptr;     // [C]
   void* mscratch = nullptr;   // [C][4][D][D] dense update workspace
+  void* zbuf = nullptr;       // [steps][C][D] momentum normals of a launch (nuts_momenta_kernel)
+  bool momentum_pass = true;  // gm_nuts_set_momentum_pass
+#ifndef GM_NUTS_ZBUF_MAX
+#define GM_NUTS_ZBUF_MAX (4ull << 30)  // at most 4 GiB (cfg3: 1 GiB per 500-transition launch)
+#endif
+  size_t zbuf_bytes = 0;
 };
 
 int nuts_init_state(NutsState* ns, gm_dtype dt, long long C, int D, int max_depth);

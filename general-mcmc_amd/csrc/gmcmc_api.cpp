@@ -1205,6 +1205,13 @@ int gm_nuts_set_mass_adaptation(gm_sampler* s, int32_t mode, int64_t start_buffe
                        regularize, jitter);
 }
 
+int gm_nuts_set_momentum_pass(gm_sampler* s, int32_t on) {
+  GM_REQ(s, "sampler is NULL");
+  GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");
+  s->nuts.momentum_pass = on != 0;
+  return GM_OK;
+}
+
 int gm_nuts_set_lds_levels(gm_sampler* s, int32_t levels) {
   GM_REQ(s, "sampler is NULL");
   GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");

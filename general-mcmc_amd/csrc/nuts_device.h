@@ -1026,14 +1026,25 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       if constexpr (MASS == 3) return v0l;
       else return v0o;
     }();
-    if (live && starting) {  // momentum (generic_nuts.rs:758-762)
-      T z[E];
+    // the transition's standard normals (generic_nuts.rs:758-762): from the
+    // launch's pre-drawn block (their loads in flight under the evaluation
+    // below), else drawn here; the metric's product after the evaluation
+    T zs[E];
+    if (live && starting) {
+      if (a.zmom != nullptr) {
+        const T* __restrict__ zm = (const T*)a.zmom + ((long long)s * C + c) * D;
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const int i = lane * E + e;
-        z[e] = (i < D) ? ncache[e].get_s(a.seed, cid, st, TAG_NUTS_MOM, (uint32_t)i) : (T)0;
+        for (int e = 0; e < E; ++e) {
+          const int i = lane * E + e;
+          zs[e] = (i < D) ? zm[i] : (T)0;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = lane * E + e;
+          zs[e] = (i < D) ? ncache[e].get_s(a.seed, cid, st, TAG_NUTS_MOM, (uint32_t)i) : (T)0;
+        }
       }
-      momentum_from<LPC, E>(M, z, p0, lane);
     }
 #ifdef GM_NUTS_PROF
     GM_PSEG(0);
@@ -1077,6 +1088,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
 #endif
 #pragma unroll
     for (int e = 0; e < E; ++e) pe[e] = pe[e] + gx[e] * h;  // (unconditionally, as above)
+    if (live && starting) momentum_from<LPC, E>(M, zs, p0, lane);  // sample_momentum (:275-303)
     T wx[E];  // dense metric: M^-1 g at the evaluation point
     {
       T pk[E];

@@ -157,6 +157,36 @@ __global__ void nuts_mass_update_kernel(long long C, int D, int mode, double reg
   }
 }
 
+// The transition momenta of a NUTS launch as standard normals, out[s][c][i]
+// for steps step0 .. step0 + n - 1: the values nuts_kernel would draw at each
+// transition start (normals_of over the (seed, chain, step / S, TAG_NUTS_MOM,
+// i) Philox blocks, S steps per block), drawn here in one fully parallel pass
+// -- every (block, chain, coordinate) at once -- instead of inside the tree
+// loop, where each draw held up the wave's other chains at their transition
+// start. Consecutive threads take consecutive coordinates (coalesced rows).
+template <class T>
+__global__ void nuts_momenta_kernel(uint64_t seed, uint32_t chain_offset, uint64_t step0, long long n, long long C,
+                                    int D, T* __restrict__ out) {
+  constexpr int S = Blk<T>::S;
+  const uint64_t b0 = step0 / S;
+  const long long nb = (long long)((step0 + (uint64_t)n - 1) / S - b0 + 1);
+  const long long total = nb * C * D;
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+       k += (long long)gridDim.x * blockDim.x) {
+    const int i = (int)(k % D);
+    const long long r = k / D;
+    const long long c = r % C;
+    const uint64_t b = b0 + (uint64_t)(r / C);
+    T z[S];
+    normals_of(draw_block(seed, chain_offset + (uint32_t)c, b, TAG_NUTS_MOM, (uint32_t)i), z);
+#pragma unroll
+    for (int u = 0; u < S; ++u) {
+      const uint64_t st = b * S + (uint64_t)u;
+      if (st >= step0 && st < step0 + (uint64_t)n) out[((long long)(st - step0) * C + c) * D + i] = z[u];
+    }
+  }
+}
+
 template <class T>
 __global__ void nuts_fill_kernel(T* eps, T* eps_bar, T* h_bar, T* mu, long long C) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -316,6 +346,7 @@ void nuts_free_state(NutsState* ns) {
   ffree(ns->stk_n);
   ffree(ns->stk_na);
   ffree(ns->n_leapfrog);
+  ffree(ns->zbuf);
   *ns = NutsState();
 }
 
@@ -508,6 +539,34 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
       a.trk.n0 = trk->n0 + (unsigned long long)start;
     }
     hipEventRecord(evs[2 * li], st);
+    // the launch's momenta in one parallel pass ahead of the tree kernel
+    // (same values; skipped past GM_NUTS_ZBUF_MAX bytes, the kernel then draws
+    // them itself), timed with the launch
+    {
+      const size_t zb = (size_t)(nst > 0 ? nst : 0) * (size_t)C * (size_t)D * esz;
+      if (ns.momentum_pass && zb > 0 && zb <= (size_t)GM_NUTS_ZBUF_MAX) {
+        if (zb > ns.zbuf_bytes) {
+          if (ns.zbuf) hipFree(ns.zbuf);
+          ns.zbuf = nullptr;
+          ns.zbuf_bytes = 0;
+          if (hipMalloc(&ns.zbuf, zb) == hipSuccess) ns.zbuf_bytes = zb;
+          else (void)hipGetLastError();  // no buffer: the kernel draws its momenta
+        }
+        if (ns.zbuf) {
+          const long long S = dt == GM_F32 ? 4 : 2;
+          const long long nb = (long long)((a.step0 + (uint64_t)nst - 1) / S - a.step0 / S + 1);
+          const long long work = nb * C * D;
+          const unsigned zbk = (unsigned)((work + 255) / 256 < 65536 ? (work + 255) / 256 : 65536);
+          if (dt == GM_F32)
+            hipLaunchKernelGGL(nuts_momenta_kernel<float>, dim3(zbk), dim3(256), 0, st, seed, chain_offset, a.step0,
+                               nst, C, D, (float*)ns.zbuf);
+          else
+            hipLaunchKernelGGL(nuts_momenta_kernel<double>, dim3(zbk), dim3(256), 0, st, seed, chain_offset,
+                               a.step0, nst, C, D, (double*)ns.zbuf);
+          a.zmom = ns.zbuf;
+        }
+      }
+    }
     hipError_t e;
     if (tg.kind == GM_TARGET_CUSTOM) {  // user target, runtime-compiled (gm_jit.cpp)
       const unsigned blocks = (unsigned)((C + 255) / 256);

@@ -112,6 +112,12 @@ class NUTS(Sampler):
         _lib.check(self._lib.gm_nuts_set_dense_forms(self._h, int(minv_lds), int(chol_lds)))
         return self
 
+    def set_momentum_pass(self, on: bool = True):
+        """Draw the transition momenta in one parallel pass per launch (the
+        default) or inside the tree kernel; identical results."""
+        _lib.check(self._lib.gm_nuts_set_momentum_pass(self._h, 1 if on else 0))
+        return self
+
     def launch_plan(self) -> dict:
         """The last launch's on-chip plan (gm_nuts_get_plan)."""
         p = np.zeros(6, dtype=np.int32)

@@ -249,6 +249,13 @@ int gm_nuts_set_dense_forms(gm_sampler* s, int32_t minv_lds, int32_t chol_lds);
  * warm-up window: GM_FROZEN_WAVES waves per SIMD). plan holds 6 values. */
 int gm_nuts_get_plan(gm_sampler* s, int32_t* plan);
 
+/* Where the NUTS transition momenta are drawn: on (default) in one parallel
+ * pass per launch ahead of the tree kernel, into a [steps][C][D] buffer (at
+ * most 4 GiB; larger launches draw in the kernel), off in the tree kernel at
+ * each transition start. The same Philox/Box-Muller values either way
+ * (identical results); no reference counterpart. */
+int gm_nuts_set_momentum_pass(gm_sampler* s, int32_t on);
+
 int gm_nuts_get_mass(gm_sampler* s, int32_t* mode, int32_t* kind, void* dinv, void* dsqrt, void* minv,
                      void* mchol);
 

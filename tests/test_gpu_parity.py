@@ -203,3 +203,27 @@ def test_split_rhat_ess_matches_oracle(gm, oracle, shape, dtype):
     np.testing.assert_allclose(r, orr, atol=1e-3)  # north-star tolerance: R-hat within 1e-3
     np.testing.assert_allclose(e, oe, rtol=1e-3)
 
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("dim,lay", [(32, (16, 2)), (7, (8, 1)), (300, (256, 2))])
+def test_nuts_momentum_pass_forms_bitwise(gm, oracle, dtype, dim, lay):
+    """The transition momenta drawn in one parallel pass per launch (the
+    default, nuts_momenta_kernel) or inside the tree kernel: the oracle's bits
+    either way, across launches of a run (steps_per_launch) and a second run."""
+    n_chains = 10
+    x0 = start(gm, n_chains, dim, dtype, 0.5)
+    t = gm.IsotropicGaussian(1.2)
+    outs = []
+    for on in (True, False):
+        s = gm.NUTS(t, x0, 0.8, dtype=dtype, max_depth=6).set_seed(21)
+        s.set_layout(*lay)
+        s.set_momentum_pass(on)
+        s.set_steps_per_launch(4)
+        outs.append((s.run(5, 6), s.run(3, 0)))
+    st = oracle.nuts_state(n_chains, dtype)
+    q, s1, _, _ = oracle.nuts_run(Target.from_product(t, dim), x0, st, 0.8, 6, 21, 0, 5, 6, False, *lay)
+    _, s2, _, _ = oracle.nuts_run(Target.from_product(t, dim), q, st, 0.8, 6, 21, 11, 3, 0, False, *lay)
+    for a, b in outs:
+        np.testing.assert_array_equal(a, s1.transpose(1, 0, 2))
+        np.testing.assert_array_equal(b, s2.transpose(1, 0, 2))
