@@ -73,6 +73,16 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
+def _build_info():
+    """The library's embedded source digest against this tree's (the loader
+    refuses a mismatch; recorded so the line names the sources it measured)."""
+    try:
+        import general_mcmc_amd as gm
+        return gm._lib.build_info()
+    except Exception as e:  # the CPU-stubbed CLI tests have no library
+        return {"error": str(e)}
+
+
 def dense_gauss_32():
     """configs[2]'s target: mean 0, Sigma = Q diag(logspace(-1, 1,
     32)) Q^T with Q from the QR of a seed-42 N(0,1) 32x32 matrix."""
@@ -910,6 +920,7 @@ def main(argv=None, backend=None):
             "rccl": comm_info,
             "north_star_check": extra.get("north_star_check"),
             "host_output": extra.get("host_output"),
+            "build": _build_info(),
         }
         print(json.dumps(line), flush=True)
     if comm is not None:

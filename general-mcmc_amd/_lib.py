@@ -157,6 +157,8 @@ def load(path: str | None = None) -> C.CDLL:
         raise GMError(GM_ESTATE, f"{p} not found: build it with `make -C general-mcmc_amd` "
                                  "(no CPU fallback exists)")
     lib = C.CDLL(p)
+    if path is None and "GMCMC_LIB" not in os.environ:
+        _check_build(lib, p)
     for name, (res, args) in SIGNATURES.items():
         if "GMCMC_LIB" in os.environ and not hasattr(lib, name):
             continue  # an A/B build of an earlier tree may predate an entry point
@@ -166,6 +168,34 @@ def load(path: str | None = None) -> C.CDLL:
     if path is None:
         _lib = lib
     return lib
+
+
+def build_info(lib=None) -> dict:
+    """The loaded library's source digest (gm_build_info, embedded at build
+    time) and the digest of the sources in this tree."""
+    lib = lib or load()
+    fn = getattr(lib, "gm_build_info", None)
+    built = None
+    if fn is not None:
+        fn.restype = C.c_char_p
+        built = fn().decode()
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_gm_source_digest", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
+                                          "source_digest.py"))
+    tree = None
+    if spec is not None and os.path.exists(spec.origin):
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        tree = "src:" + mod.digest()
+    return {"library": built, "tree": tree, "match": built is not None and built == tree}
+
+
+def _check_build(lib, p) -> None:
+    info = build_info(lib)
+    if info["tree"] is not None and not info["match"]:
+        raise GMError(GM_ESTATE, f"{p} was built from other sources ({info['library']}) than this tree's "
+                                 f"({info['tree']}): rebuild with `make -C general-mcmc_amd`")
 
 
 def check(rc: int) -> None:
