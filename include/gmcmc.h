@@ -112,6 +112,11 @@ int gm_init_positions_rows(uint64_t seed, int64_t row0, int64_t n, int64_t dim, 
 
 /* ---- device / errors ------------------------------------------------ */
 const char* gm_last_error(void);
+
+/* "src:<digest>": the digest of the sources this library was built from
+ * (tools/source_digest.py over csrc/, this header and the Makefile); the
+ * Python layer refuses a library whose digest differs from its tree's. */
+const char* gm_build_info(void);
 int gm_device_count(int* count);
 /* Select the calling thread's device. Called before the device is first used,
  * it also makes the thread's host waits spin (hipDeviceScheduleSpin): run
