@@ -91,6 +91,7 @@ SIGNATURES = {
     "gm_nuts_set_dense_forms": (_ip, [_vp, _i32, _i32]),
     "gm_nuts_get_plan": (_ip, [_vp, _vp]),
     "gm_nuts_set_momentum_pass": (_ip, [_vp, _i32]),
+    "gm_build_info": (C.c_char_p, []),
     "gm_nuts_get_mass": (_ip, [_vp, C.POINTER(_i32), _vp, _vp, _vp, _vp, _vp]),
     "gm_sampler_layout": (_ip, [_vp, C.POINTER(_i32), C.POINTER(_i32)]),
     "gm_sampler_set_layout": (_ip, [_vp, _i32, _i32]),
