@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
     tblk[e] = ~0ull;
   }
   UniformCache<T> ucache;
-  uint64_t lblk = ~0ull;  // LPC == 64: the draw block whose accept logs lnl holds (lane k: step k)
+  uint64_t lblk = ~0ull;  // LPC == 64: the 64-step window whose accept logs lnl holds (lane k: step 64 lblk + k)
   T lnl = (T)0;
   const bool track = a.trk.mean != nullptr;  // run_progress (core.rs:146-163)
   ChainTrack<LPC, E> tr;
@@ -100,21 +100,22 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
     const T log_alpha = (lp1 + logq) - (lp + logq);
     T lnu;
     if constexpr (LPC == 64) {
-      // the accept log-uniforms of a whole draw block in one VALU pass: lane
-      // k evaluates ln u_k of the block (wave-uniform inputs), the step reads
-      // lane st % S back as a scalar (the HMC draw block's form)
+      // the accept log-uniforms of 64 consecutive steps in one VALU pass:
+      // lane k evaluates ln u of step 64 m + k (its draw block and word), and
+      // each step reads lane st % 64 back as a scalar
       constexpr int S = Blk<T>::S;
-      const uint64_t b = st / S;
+      const uint64_t b = st / 64;
       if (b != lblk) {
+        const uint64_t sk = b * 64 + (uint64_t)lane;
         T us[S];
-        uniforms_of(draw_block(a.seed, ucid, b, TAG_MH_ACC, 0u), us);
+        uniforms_of(draw_block(a.seed, ucid, sk / S, TAG_MH_ACC, 0u), us);
         T um = us[0];
 #pragma unroll
         for (int k = 1; k < S; ++k) um = ((lane & (S - 1)) == k) ? us[k] : um;
         lnl = glog_unif(um);
         lblk = b;
       }
-      lnu = lane_k(lnl, (int)(st % S));
+      lnu = lane_k(lnl, (int)(st % 64));
     } else {
       lnu = glog_unif(ucache.get(a.seed, ucid, st, TAG_MH_ACC, 0u));
     }
