@@ -244,6 +244,25 @@ template <class T> __device__ __forceinline__ T div_by_const(T a, T b, T y) {
   return q2;
 }
 
+// div_by_const without its range branch: q2, and `bad` set when |q2| is
+// outside the exponent range where q2 is proven the IEEE quotient (biased
+// exponent 23 ... 2022, i.e. [2^-1000, 2^1000), zero, subnormals, inf and NaN
+// excluded): the caller tests one flag for several quotients and divides
+// in its rare branch.
+template <class T> __device__ __forceinline__ T div_by_const_q(T a, T b, T y, bool& bad) {
+  const T q0 = a * y;
+  const T q1 = gfma(gfma(-b, q0, a), y, q0);
+  const T q2 = gfma(gfma(-b, q1, a), y, q1);
+  if constexpr (sizeof(T) == 8) {
+    const uint32_t ex = (uint32_t)(__builtin_bit_cast(uint64_t, q2) >> 52) & 0x7FFu;
+    bad |= ex - 23u > 1999u;
+  } else {
+    const uint32_t ex = (__builtin_bit_cast(uint32_t, q2) >> 23) & 0xFFu;  // [2^-99, 2^99)
+    bad |= ex - 28u > 197u;
+  }
+  return q2;
+}
+
 template <class T, int E> struct RosenbrockLane;
 template <class T> struct RosenbrockT {
   T a, b, b2, b4;  // b2 = 2b, b4 = 4b (rounded once, host side)

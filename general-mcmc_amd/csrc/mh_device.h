@@ -6,6 +6,10 @@
 #include "gm_launch.h"
 #include "gm_track.h"
 
+#ifndef GM_MH_QCHK
+#define GM_MH_QCHK 1
+#endif
+
 namespace gm {
 
 template <class T, int LPC, int E, class TG>
@@ -48,12 +52,9 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   // f64: the table-driven Box-Muller pair of each coordinate's current block
   // (two steps), as plain per-coordinate values (selected, never indexed)
   double tz0[E], tz1[E];
-  uint64_t tblk[E];
+  uint64_t tb = ~0ull;  // the block index (st / 2) the pairs belong to
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    tz0[e] = tz1[e] = 0.0;
-    tblk[e] = ~0ull;
-  }
+  for (int e = 0; e < E; ++e) tz0[e] = tz1[e] = 0.0;
   UniformCache<T> ucache;
   uint64_t lblk = ~0ull;  // LPC == 64: the 64-step window whose accept logs lnl holds (lane k: step 64 lblk + k)
   T lnl = (T)0;
@@ -63,18 +64,24 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   for (int s = 0; s < a.n_steps; ++s) {
     const uint64_t st = a.step0 + (uint64_t)s;
     T qpart = (T)0;
+#if GM_MH_QCHK
+    T ex[E];
+    bool qbad = false;
+#endif
+    // f64: the coordinates' pairs are all fresh at the same steps (the block
+    // index is the lane-independent st / 2), one wave-uniform test
+    const bool fresh = TAB && (st / 2 != tb);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
       if (i < D) {
         T n;
         if constexpr (TAB) {
-          if (st / 2 != tblk[e]) {
+          if (fresh) {
             double z[2];
-            normals_tab(draw_block(a.seed, cid, st / 2, TAG_MH_PROP, (uint32_t)i), z, bm_lds[0]);
+            normals_tab(draw_block_v(a.seed, cid, st / 2, TAG_MH_PROP, (uint32_t)i), z, bm_lds[0]);
             tz0[e] = z[0];
             tz1[e] = z[1];
-            tblk[e] = st / 2;
           }
           n = (st & 1u) ? tz1[e] : tz0[e];
         }
@@ -85,9 +92,29 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
       }
       const T d = y[e] - x[e];
       // -(d*d) / two_var (distributions.rs:385), the IEEE quotient exactly
+#if GM_MH_QCHK
+      // its fast form for every coordinate first, one range test for the
+      // lane's E quotients (div_by_const_q), the IEEE division in a branch
+      // no wave meets in practice
+      ex[e] = (i < D) ? div_by_const_q(-(d * d), two_var, inv_two_var, qbad) : (T)0;
+#else
       const T ex = (i < D) ? div_by_const(-(d * d), two_var, inv_two_var) : (T)0;
       qpart = (e == 0) ? ex : qpart + ex;
+#endif
     }
+    if constexpr (TAB) tb = st / 2;
+#if GM_MH_QCHK
+    if (__builtin_expect(qbad, 0)) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        const T d = y[e] - x[e];
+        if (i < D) ex[e] = -(d * d) / two_var;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) qpart = (e == 0) ? ex[e] : qpart + ex[e];
+#endif
     // the proposal density's sum and the target's, reduced together: the
     // same stages (and bits) as two group_sums, each stage's DPP latency
     // covered by the other sum instead of wait states
@@ -108,7 +135,7 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
       if (b != lblk) {
         const uint64_t sk = b * 64 + (uint64_t)lane;
         T us[S];
-        uniforms_of(draw_block(a.seed, ucid, sk / S, TAG_MH_ACC, 0u), us);
+        uniforms_of(draw_block_v(a.seed, ucid, sk / S, TAG_MH_ACC, 0u), us);
         T um = us[0];
 #pragma unroll
         for (int k = 1; k < S; ++k) um = ((lane & (S - 1)) == k) ? us[k] : um;
