@@ -148,6 +148,29 @@ def test_mh_samples_bitwise(gm, oracle, dtype, dim, lay):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("std", [1e-30, 1e-6, 3.0])
+def test_mh_exact_quotient_edges_bitwise(gm, oracle, dtype, std):
+    """The proposal density's -(d*d)/(2 sd^2) outside the fast quotient's
+    proven range takes the IEEE division (mh_device.h, div_by_const_q): sd
+    1e-30 gives d = 0 (x + n sd == x) for every coordinate, so every step
+    divides -0 (and in f32 sd^2 underflows to 0, so the quotient is NaN);
+    1e-6 and 3 are in-range controls. 64 x 4 and 32 x 8 at 256 dimensions,
+    as cfg5."""
+    dim, n_chains = 256, 12
+    x0 = start(gm, n_chains, dim, dtype, 1.0)
+    t = gm.IsotropicGaussian(1.0)
+    prop = gm.IsotropicGaussian(std)
+    for lay in ((64, 4), (32, 8)):
+        s = gm.MetropolisHastings(t, prop, x0, dtype=dtype).seed(11)
+        s.set_layout(*lay)
+        out = s.run(6, 3)
+        q, samples, acc = oracle.mh_run(Target.from_product(t, dim), x0, prop.std, 11, 0, 9, 3, *lay)
+        np.testing.assert_array_equal(out, samples.transpose(1, 0, 2).astype(np.float64), err_msg=str(lay))
+        np.testing.assert_array_equal(s.accept_counts(), acc, err_msg=str(lay))
+        s.close()
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("dim,lay", [(2, (2, 1)), (5, (8, 1)), (32, (32, 1)), (32, (16, 2))])
 @pytest.mark.parametrize("progress", [False, True])
 @pytest.mark.parametrize("lds_levels", [-1, 0, 2])  # subtree stack in LDS / HBM / split
