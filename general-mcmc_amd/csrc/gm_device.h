@@ -104,6 +104,28 @@ template <int LPC, int N, class T> __device__ __forceinline__ void block_totals(
   __syncthreads();  // red is reused by the next sum
 }
 
+// v + (the value of lane l ^ 16): rows r and r ^ 1 exchanged by one
+// v_permlane16_swap per 32-bit half (a VALU op) instead of __shfl_xor's LDS
+// round trip (ds_bpermute); the pair sum is the same in both rows (IEEE
+// addition commutes), as with the shuffle.
+__device__ __forceinline__ float xor16_sum(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+__device__ __forceinline__ double xor16_sum(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)u, (unsigned)u, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
+  const double a = __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi[0] << 32) | (unsigned)lo[0]);
+  const double b = __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi[1] << 32) | (unsigned)lo[1]);
+  return a + b;
+}
+__device__ __forceinline__ int xor16_sum(int v) {
+  const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  return (int)r[0] + (int)r[1];
+}
+
 template <int LPC, class T> __device__ __forceinline__ T group_sum(T v) {
   if constexpr (LPC > 64) {
     T t[1] = {group_sum<64>(v)};
@@ -114,7 +136,7 @@ template <int LPC, class T> __device__ __forceinline__ T group_sum(T v) {
   if constexpr (LPC >= 4) v = v + dpp<DPP_QUAD_XOR2>(v);
   if constexpr (LPC >= 8) v = v + dpp<DPP_ROW_HALF_MIRROR>(v);
   if constexpr (LPC >= 16) v = v + dpp<DPP_ROW_MIRROR>(v);
-  if constexpr (LPC == 32) v = v + __shfl_xor(v, 16, 64);
+  if constexpr (LPC == 32) v = xor16_sum(v);
   if constexpr (LPC >= 64) {
     // Every lane of row r now holds the row total r_r. Rows 1 and 3 add the
     // broadcast of rows 0 and 2 (r1+r0, r3+r2), then row 3 adds row 1's value:
@@ -146,7 +168,7 @@ template <int LPC, int N, class T> __device__ __forceinline__ void group_sum_n(T
   GM_STAGE(LPC >= 4, v[k] + dpp<DPP_QUAD_XOR2>(v[k]))
   GM_STAGE(LPC >= 8, v[k] + dpp<DPP_ROW_HALF_MIRROR>(v[k]))
   GM_STAGE(LPC >= 16, v[k] + dpp<DPP_ROW_MIRROR>(v[k]))
-  GM_STAGE(LPC == 32, v[k] + __shfl_xor(v[k], 16, 64))
+  GM_STAGE(LPC == 32, xor16_sum(v[k]))
   GM_STAGE(LPC >= 64, v[k] + (dpp_rows<DPP_ROW_BCAST15, 0xa>(v[k])))
   GM_STAGE(LPC >= 64, v[k] + (dpp_rows<DPP_ROW_BCAST31, 0x8>(v[k])))
   GM_STAGE(LPC >= 64, lane63(v[k]))
