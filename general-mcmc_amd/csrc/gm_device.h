@@ -252,25 +252,11 @@ __device__ __forceinline__ double gfma(double a, double b, double c) { return __
 // (the remainder exact by fma) is faithful; a second one, q2, is then the
 // correctly rounded quotient (Markstein's theorem: y within half an ulp of
 // 1/b and a faithful q). The theorem excludes under/overflow and non-finite
-// a: those inputs (|a/b| outside [2^-1000, 2^1000], a = 0, inf, NaN) take
-// the IEEE division itself, in a branch no wave of the samplers reaches in
-// practice; a = 0 keeps its sign through that branch too.
-template <class T> __device__ __forceinline__ T div_by_const(T a, T b, T y) {
-  const T q0 = a * y;
-  const T q1 = gfma(gfma(-b, q0, a), y, q0);
-  const T q2 = gfma(gfma(-b, q1, a), y, q1);
-  const T m = q2 < (T)0 ? -q2 : q2;
-  constexpr T lo = sizeof(T) == 8 ? (T)9.332636185032189e-302 : (T)1e-30f;  // 2^-1000 | 1e-30
-  constexpr T hi = sizeof(T) == 8 ? (T)1.0715086071862673e+301 : (T)1e30f;  // 2^1000  | 1e30
-  if (__builtin_expect(!(m >= lo && m <= hi), 0)) return a / b;
-  return q2;
-}
-
-// div_by_const without its range branch: q2, and `bad` set when |q2| is
-// outside the exponent range where q2 is proven the IEEE quotient (biased
-// exponent 23 ... 2022, i.e. [2^-1000, 2^1000), zero, subnormals, inf and NaN
-// excluded): the caller tests one flag for several quotients and divides
-// in its rare branch.
+// a, so q2 is returned with `bad` set when |q2| is outside the exponent range
+// where it is proven (biased exponent 23 ... 2022, i.e. [2^-1000, 2^1000);
+// zero, subnormals, inf and NaN excluded): the caller tests one flag for
+// several quotients and takes the IEEE division in its rare branch (a = 0
+// then keeps its sign).
 template <class T> __device__ __forceinline__ T div_by_const_q(T a, T b, T y, bool& bad) {
   const T q0 = a * y;
   const T q1 = gfma(gfma(-b, q0, a), y, q0);

@@ -563,9 +563,6 @@ __device__ __forceinline__ void bm_lds_fill(BmLds& t) {
     t.sc[k] = gm_bm_d2{gm_bm_sincos[2 * k], gm_bm_sincos[2 * k + 1]};
   }
 }
-#ifndef GM_BM_FAST
-#define GM_BM_FAST 1
-#endif
 // sqrt(x) for x = 0 or 2^-767 <= x < inf: LLVM's gfx950 f64 sequence (rsq, a
 // Goldschmidt step, two Newton corrections) without its small-input scaling,
 // which is the identity on that range; the same bits as gsqrt there.
@@ -583,7 +580,6 @@ __device__ __forceinline__ double sqrt_unscaled(double x) {
 }
 __device__ __forceinline__ void normals_tab(u32x4 x, double (&z)[2], const BmLds& t) {
   // ln u1
-#if GM_BM_FAST
   // u1 = (k + 1) 2^-53, k = (x >> 5) 2^26 + (y >> 6) (Unif<double>::oc) without
   // integer-to-double conversions: D = 2^52 + (k >> 1) assembled from its bits,
   // then u1 = fma(D, 2^-52, c), c = -1 + (1 + (k & 1)) 2^-53; the product and
@@ -591,9 +587,6 @@ __device__ __forceinline__ void normals_tab(u32x4 x, double (&z)[2], const BmLds
   const double D1 = u2d(((uint64_t)(0x43300000u | (x.x >> 12)) << 32) |
                         (((x.x << 20) & 0xFE000000u) | (x.y >> 7)));
   const double u1 = __builtin_fma(D1, 0x1p-52, u2d((x.y & 64u) ? 0xBFEFFFFFFFFFFFFEull : 0xBFEFFFFFFFFFFFFFull));
-#else
-  const double u1 = Unif<double>::oc(x.x, x.y);
-#endif
   const uint64_t b = d2u(u1);
   const int e = (int)(b >> 52) - 1023;
   const uint64_t mb = b & 0x000fffffffffffffull;
@@ -609,7 +602,6 @@ __device__ __forceinline__ void normals_tab(u32x4 x, double (&z)[2], const BmLds
   const double lnu = __builtin_fma(de, 0x1.62e42fefa39efp-1, __builtin_fma(de, 0x1.abc9e3b39803fp-56, lc.y + l1));
   // clamped at +0: for u1 = 1 (probability 2^-53) ln u1 rounds to +1.6e-17
   const double m2l = -2.0 * lnu;
-#if GM_BM_FAST
   // -2 ln u1 is 0 (clamped) or >= 2^-52 (u1 <= 1 - 2^-53)
   const double rad = sqrt_unscaled(m2l > 0.0 ? m2l : 0.0);
   // sin / cos of 2 pi u2, u2 = k2 2^-53 (Unif<double>::co): j = floor(256 u2)
@@ -620,13 +612,6 @@ __device__ __forceinline__ void normals_tab(u32x4 x, double (&z)[2], const BmLds
   const double D2 = u2d(((uint64_t)(0x43300000u | ((x.z >> 11) & 0x1FFFu)) << 32) |
                         (((x.z << 21) & 0xFC000000u) | (x.w >> 6)));
   const double th = __builtin_fma(D2, 0x1.921fb54442d18p-51, -0x1.921fb54442d18p+1);
-#else
-  const double rad = gsqrt(m2l > 0.0 ? m2l : 0.0);
-  // sin / cos of 2 pi u2
-  const double u2 = Unif<double>::co(x.z, x.w);
-  const int j = (int)(u2 * 256.0);
-  const double th = (u2 - (double)j * 0.00390625) * 0x1.921fb54442d18p+2;
-#endif
   const double zz = th * th;
   const double sth = __builtin_fma(th * zz, __builtin_fma(zz, __builtin_fma(zz, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7),
                                                           -0x1.5555555555555p-3), th);

@@ -6,10 +6,6 @@
 #include "gm_launch.h"
 #include "gm_track.h"
 
-#ifndef GM_MH_QCHK
-#define GM_MH_QCHK 1
-#endif
-
 namespace gm {
 
 template <class T, int LPC, int E, class TG>
@@ -36,7 +32,7 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   const T sd = (T)a.prop_std;
   const T var = sd * sd;
   const T two_var = (T)2 * var;
-  const T inv_two_var = (T)1 / two_var;  // div_by_const: the exact quotient by two_var
+  const T inv_two_var = (T)1 / two_var;  // div_by_const_q: the exact quotient by two_var
   const T pi = (T)3.14159265358979323846;
   const T qconst = (-(T)D * (T)0.5) * glog(((var * pi) * sd) * sd);
 
@@ -64,10 +60,8 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   for (int s = 0; s < a.n_steps; ++s) {
     const uint64_t st = a.step0 + (uint64_t)s;
     T qpart = (T)0;
-#if GM_MH_QCHK
     T ex[E];
     bool qbad = false;
-#endif
     // f64: the coordinates' pairs are all fresh at the same steps (the block
     // index is the lane-independent st / 2), one wave-uniform test
     const bool fresh = TAB && (st / 2 != tb);
@@ -92,18 +86,12 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
       }
       const T d = y[e] - x[e];
       // -(d*d) / two_var (distributions.rs:385), the IEEE quotient exactly
-#if GM_MH_QCHK
       // its fast form for every coordinate first, one range test for the
       // lane's E quotients (div_by_const_q), the IEEE division in a branch
       // no wave meets in practice
       ex[e] = (i < D) ? div_by_const_q(-(d * d), two_var, inv_two_var, qbad) : (T)0;
-#else
-      const T ex = (i < D) ? div_by_const(-(d * d), two_var, inv_two_var) : (T)0;
-      qpart = (e == 0) ? ex : qpart + ex;
-#endif
     }
     if constexpr (TAB) tb = st / 2;
-#if GM_MH_QCHK
     if (__builtin_expect(qbad, 0)) {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -114,7 +102,6 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
     }
 #pragma unroll
     for (int e = 0; e < E; ++e) qpart = (e == 0) ? ex[e] : qpart + ex[e];
-#endif
     // the proposal density's sum and the target's, reduced together: the
     // same stages (and bits) as two group_sums, each stage's DPP latency
     // covered by the other sum instead of wait states
