@@ -9,7 +9,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; rev=$2
 OUT=$ROOT/abtest/$name; SRC=$(mktemp -d)
 mkdir -p "$OUT"
-(cd "$ROOT" && git archive "$rev" general-mcmc_amd include tools/embed_headers.py | tar -x -C "$SRC")
+(cd "$ROOT" && git archive "$rev" general-mcmc_amd include tools/embed_headers.py tools/source_digest.py | tar -x -C "$SRC")
 make -s -C "$SRC/general-mcmc_amd" -j8 LIB="$OUT/libgmcmc.so" >/dev/null
 rm -rf "$SRC"
 echo "built abtest/$name from $rev"
