@@ -634,7 +634,7 @@ def load_pmc_config(name):
     return {"transitions_per_launch": int(k), "launch_us_traced": r.get("launch_us_traced"),
             "hbm_bytes_per_launch": r.get("hbm_bytes_per_launch"), "issue_frac": v.get("issue_frac"),
             "valu_insts_per_wave": v.get("valu_insts_per_wave"), "salu_per_valu": v.get("salu_per_valu"),
-            "wave_wait_frac": v.get("wave_wait_frac"), "source": r.get("source")}
+            "wave_wait_frac": v.get("wave_wait_frac"), "clock_ghz": v.get("clock_ghz"), "source": r.get("source")}
 
 
 def config_summary(name, cfg, figs, world, rhat, ess):
