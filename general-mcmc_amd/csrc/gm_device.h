@@ -506,58 +506,85 @@ template <class T, int E> struct RosenbrockLane {
 
 // IsotropicGaussian as a target (distributions.rs:398-406):
 //   logp = (-0.5 * sum x^2) / (std*std),  g = (-x) / (std*std)
+// The quotients are the IEEE ones, taken by div_by_const_q with the
+// reciprocal computed once per kernel (bind), the division itself only in
+// the branch for the fast form's excluded range.
+template <class T> struct IsoGaussLane;
 template <class T> struct IsoGaussT {
   T var;  // std*std
   int D;
   template <int LPC, int E> __host__ __device__ size_t lds_bytes() const { return 0; }
-  template <int LPC, int E> __device__ __forceinline__ IsoGaussT bind(int) const { return *this; }
+  template <int LPC, int E> __device__ __forceinline__ IsoGaussLane<T> bind(int) const;
+};
+template <class T> struct IsoGaussLane {
+  T var, iv;  // std*std and RN(1 / var)
+  int D;
+  // g = (-x) / var for the coordinates i0 + e < D, +0 past D
+  template <int E> __device__ __forceinline__ void grad(const T (&x)[E], T (&g)[E], int i0) const {
+    bool bad = false;
+#pragma unroll
+    for (int e = 0; e < E; ++e) g[e] = (i0 + e < D) ? div_by_const_q(-x[e], var, iv, bad) : (T)0;
+    if (__builtin_expect(bad, 0)) {
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        if (i0 + e < D) g[e] = (-x[e]) / var;
+    }
+  }
+  __device__ __forceinline__ T quot(T a) const {
+    bool bad = false;
+    T q = div_by_const_q(a, var, iv, bad);
+    if (__builtin_expect(bad, 0)) q = a / var;
+    return q;
+  }
   // unreduced term sum x^2 of this lane; logp = finish(group_sum(part))
   template <int LPC> static constexpr bool has_part = true;
   template <int LPC, int E>
   __device__ __forceinline__ T eval_part(const T (&x)[E], T (&g)[E], int lane) const {
+    grad<E>(x, g, lane * E);
     T part = (T)0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int i = lane * E + e;
-      g[e] = (i < D) ? (-x[e]) / var : (T)0;
-      const T s = (i < D) ? x[e] * x[e] : (T)0;
+      const T s = (lane * E + e < D) ? x[e] * x[e] : (T)0;
       part = (e == 0) ? s : part + s;
     }
     return part;
   }
-  __device__ __forceinline__ T finish(T total) const { return ((T)-0.5 * total) / var; }
+  __device__ __forceinline__ T finish(T total) const { return quot((T)-0.5 * total); }
   template <int LPC, int E, bool LOGP>
   __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int lane) const {
+    grad<E>(x, g, lane * E);
+    if (!LOGP) return (T)0;
     T part = (T)0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int i = lane * E + e;
-      g[e] = (i < D) ? (-x[e]) / var : (T)0;
-      if (LOGP) {
-        const T s = (i < D) ? x[e] * x[e] : (T)0;
-        part = (e == 0) ? s : part + s;
-      }
+      const T s = (lane * E + e < D) ? x[e] * x[e] : (T)0;
+      part = (e == 0) ? s : part + s;
     }
-    if (LOGP) return ((T)-0.5 * group_sum<LPC>(part)) / var;
-    return (T)0;
+    return quot((T)-0.5 * group_sum<LPC>(part));
   }
   template <int E, bool LOGP>
   __device__ __forceinline__ T eval_wide(const T (&x)[E], T (&g)[E], WideCtx<T>& c) const {
     const int t0 = (c.w * 64 + c.lane) * E;
+    grad<E>(x, g, t0);
+    if (!LOGP) return (T)0;
     T part = (T)0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const int i = t0 + e;
-      g[e] = (i < D) ? (-x[e]) / var : (T)0;
-      if (LOGP) {
-        const T s = (i < D) ? x[e] * x[e] : (T)0;
-        part = (e == 0) ? s : part + s;
-      }
+      const T s = (t0 + e < D) ? x[e] * x[e] : (T)0;
+      part = (e == 0) ? s : part + s;
     }
-    if (LOGP) return ((T)-0.5 * block_sum(part, c)) / var;
-    return (T)0;
+    return quot((T)-0.5 * block_sum(part, c));
   }
 };
+template <class T>
+template <int LPC, int E>
+__device__ __forceinline__ IsoGaussLane<T> IsoGaussT<T>::bind(int) const {
+  IsoGaussLane<T> r;
+  r.var = var;
+  r.iv = (T)1 / var;
+  r.D = D;
+  return r;
+}
 
 // Dense Gaussian (DiffableGaussian2D generalised, distributions.rs:257-292):
 //   d = x - mu; w_k = sum_j P_kj d_j; logp = nc - 0.5*sum_k w_k d_k;

@@ -133,7 +133,10 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
     } else {
       lnu = glog_unif(ucache.get(a.seed, ucid, st, TAG_MH_ACC, 0u));
     }
-    if (log_alpha > lnu) {
+    // (one chain per wave: a wave-uniform decision, so the accepted copy is
+    // a scalar branch, not a select per register every step)
+    const bool accept = log_alpha > lnu;
+    if (LPC == 64 ? (__builtin_amdgcn_readfirstlane((int)accept) != 0) : accept) {
 #pragma unroll
       for (int e = 0; e < E; ++e) x[e] = y[e];
       lp = lp1;
