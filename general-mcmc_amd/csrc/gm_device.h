@@ -530,6 +530,16 @@ template <class T> struct IsoGaussLane {
         if (i0 + e < D) g[e] = (-x[e]) / var;
     }
   }
+  // this lane's sum of x^2 over its E slots. No mask for the padded slots:
+  // every sampler keeps a padded coordinate at +0 (loaded as +0, its momentum
+  // and gradient +0), and +0 * +0 = +0 added to a sum of squares (never -0)
+  // changes no bit, so the sum is the masked one's.
+  template <int E> __device__ __forceinline__ T sq_part(const T (&x)[E]) const {
+    T part = x[0] * x[0];
+#pragma unroll
+    for (int e = 1; e < E; ++e) part = part + x[e] * x[e];
+    return part;
+  }
   __device__ __forceinline__ T quot(T a) const {
     bool bad = false;
     T q = div_by_const_q(a, var, iv, bad);
@@ -541,39 +551,21 @@ template <class T> struct IsoGaussLane {
   template <int LPC, int E>
   __device__ __forceinline__ T eval_part(const T (&x)[E], T (&g)[E], int lane) const {
     grad<E>(x, g, lane * E);
-    T part = (T)0;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const T s = (lane * E + e < D) ? x[e] * x[e] : (T)0;
-      part = (e == 0) ? s : part + s;
-    }
-    return part;
+    return sq_part<E>(x);
   }
   __device__ __forceinline__ T finish(T total) const { return quot((T)-0.5 * total); }
   template <int LPC, int E, bool LOGP>
   __device__ __forceinline__ T eval(const T (&x)[E], T (&g)[E], int lane) const {
     grad<E>(x, g, lane * E);
     if (!LOGP) return (T)0;
-    T part = (T)0;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const T s = (lane * E + e < D) ? x[e] * x[e] : (T)0;
-      part = (e == 0) ? s : part + s;
-    }
-    return quot((T)-0.5 * group_sum<LPC>(part));
+    return quot((T)-0.5 * group_sum<LPC>(sq_part<E>(x)));
   }
   template <int E, bool LOGP>
   __device__ __forceinline__ T eval_wide(const T (&x)[E], T (&g)[E], WideCtx<T>& c) const {
     const int t0 = (c.w * 64 + c.lane) * E;
     grad<E>(x, g, t0);
     if (!LOGP) return (T)0;
-    T part = (T)0;
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const T s = (t0 + e < D) ? x[e] * x[e] : (T)0;
-      part = (e == 0) ? s : part + s;
-    }
-    return quot((T)-0.5 * block_sum(part, c));
+    return quot((T)-0.5 * block_sum(sq_part<E>(x), c));
   }
 };
 template <class T>
