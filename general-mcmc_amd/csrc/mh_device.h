@@ -85,10 +85,10 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
         y[e] = (T)0;
       }
       const T d = y[e] - x[e];
-      // -(d*d) / two_var (distributions.rs:385), the IEEE quotient exactly
-      // its fast form for every coordinate first, one range test for the
-      // lane's E quotients (div_by_const_q), the IEEE division in a branch
-      // no wave meets in practice
+      // -(d*d) / two_var (distributions.rs:385), the IEEE quotient: its fast
+      // form for every coordinate first (div_by_const_q), one range test for
+      // the lane's E quotients, the IEEE division in a branch no wave meets
+      // in practice
       ex[e] = (i < D) ? div_by_const_q(-(d * d), two_var, inv_two_var, qbad) : (T)0;
     }
     if constexpr (TAB) tb = st / 2;
