@@ -68,21 +68,18 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
-      if (i < D) {
-        T n;
-        if constexpr (TAB) {
-          if (fresh) {
-            double z[2];
-            normals_tab(draw_block_v(a.seed, cid, st / 2, TAG_MH_PROP, (uint32_t)i), z, bm_lds[0]);
-            tz0[e] = z[0];
-            tz1[e] = z[1];
-          }
-          n = (st & 1u) ? tz1[e] : tz0[e];
+      if constexpr (TAB) {
+        // (a padded slot keeps its pair at +0, so its y = +0 + +0 * sd = +0:
+        // no branch around the proposal, only around the draw)
+        if (fresh && i < D) {
+          double z[2];
+          normals_tab(draw_block_v(a.seed, cid, st / 2, TAG_MH_PROP, (uint32_t)i), z, bm_lds[0]);
+          tz0[e] = z[0];
+          tz1[e] = z[1];
         }
-        else n = ncache[e].get(a.seed, cid, st, TAG_MH_PROP, (uint32_t)i);
-        y[e] = x[e] + n * sd;
+        y[e] = x[e] + ((st & 1u) ? tz1[e] : tz0[e]) * sd;
       } else {
-        y[e] = (T)0;
+        y[e] = (i < D) ? x[e] + ncache[e].get(a.seed, cid, st, TAG_MH_PROP, (uint32_t)i) * sd : (T)0;
       }
       const T d = y[e] - x[e];
       // -(d*d) / two_var (distributions.rs:385), the IEEE quotient: its fast
