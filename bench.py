@@ -576,6 +576,8 @@ def load_pmc(C, D, L, dtype, steps):
         r = byk[steps]
         traffic = {"bytes": r["hbm_bytes_per_launch"], "source": r["source"], "scaled": False}
         issue = dict(r.get("valu", {}), scaled=False) if r.get("valu") else None
+        if issue is not None and r.get("pmc_flops") and r.get("launch_us_traced"):
+            issue["executed"] = pmc_executed(r, VALU_F32_PEAK_TFLOPS, "fp32_lane_flops")
     elif "fit" in e:
         f = e["fit"]
         traffic = {"bytes": f["fixed_bytes"] + f["bytes_per_transition"] * steps,
@@ -620,6 +622,18 @@ def f_alg_mh(D):
     return 10 * D + 6
 
 
+def pmc_executed(r, peak, key):
+    """The hardware's own flop count of a profiled dispatch (SQ_INSTS_VALU_
+    FLOPS_FP32/FP64 x 64: every lane-flop the VALU executed, FMA as 2, the RNG
+    and bookkeeping included, padded lanes excluded) over its traced time,
+    against the vector peak: the executed-flop fraction, beside the F_alg
+    fraction that counts only the algorithm's flops."""
+    fl = r["pmc_flops"][key]
+    tf = fl / (r["launch_us_traced"] * 1e-6) / 1e12
+    return {"lane_flops_per_launch": fl, "tflops": tf, "frac": tf / peak,
+            "note": "SQ_INSTS_VALU_FLOPS x 64 of the profiled dispatch / its traced duration, vs the vector peak"}
+
+
 def load_pmc_config(name):
     """PMC figures of a config leg's dispatch (profiles/r04/pmc_configs.json,
     tools/profile_r04.sh), or None."""
@@ -631,7 +645,13 @@ def load_pmc_config(name):
         return None
     k, r = next(iter(e["by_steps"].items()))
     v = r.get("valu", {})
+    ex = None
+    if r.get("pmc_flops") and r.get("launch_us_traced"):
+        f64 = r["pmc_flops"].get("fp64_lane_flops", 0.0) > 0
+        ex = pmc_executed(r, VALU_F64_PEAK_TFLOPS if f64 else VALU_F32_PEAK_TFLOPS,
+                          "fp64_lane_flops" if f64 else "fp32_lane_flops")
     return {"transitions_per_launch": int(k), "launch_us_traced": r.get("launch_us_traced"),
+            "executed_flops": ex,
             "hbm_bytes_per_launch": r.get("hbm_bytes_per_launch"), "issue_frac": v.get("issue_frac"),
             "valu_insts_per_wave": v.get("valu_insts_per_wave"), "salu_per_valu": v.get("salu_per_valu"),
             "wave_wait_frac": v.get("wave_wait_frac"), "clock_ghz": v.get("clock_ghz"), "source": r.get("source")}
@@ -906,6 +926,7 @@ def main(argv=None, backend=None):
                                  "of the launch: the collected samples plus one state read/write)",
                          "traffic_source": traffic,
                          "valu_issue": issue,
+                         "pmc_flops_frac": (issue or {}).get("executed", {}).get("frac"),
                          "hbm_equivalent": {"achieved_gbs": hbm_gbs, "peak_gbs": HBM_PEAK_GBS,
                                             "hbm_equivalent_frac": hbm_gbs / HBM_PEAK_GBS,
                                             "algorithmic_bytes_per_launch": hbm_bytes,

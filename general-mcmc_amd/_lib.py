@@ -89,7 +89,7 @@ SIGNATURES = {
     "gm_nuts_set_mass_adaptation": (_ip, [_vp, _i32, _i64, _i64, _i64, _dbl, _dbl, _i64]),
     "gm_nuts_set_lds_levels": (_ip, [_vp, _i32]),
     "gm_nuts_set_dense_forms": (_ip, [_vp, _i32, _i32]),
-    "gm_nuts_get_plan": (_ip, [_vp, _vp]),
+    "gm_nuts_get_plan": (_ip, [_vp, _vp, _i32]),
     "gm_nuts_set_momentum_pass": (_ip, [_vp, _i32]),
     "gm_build_info": (C.c_char_p, []),
     "gm_nuts_get_mass": (_ip, [_vp, C.POINTER(_i32), _vp, _vp, _vp, _vp, _vp]),

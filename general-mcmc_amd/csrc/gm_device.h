@@ -249,24 +249,52 @@ __device__ __forceinline__ double gfma(double a, double b, double c) { return __
 // the IEEE quotient RN(a/b) in one multiply and four fused multiply-adds
 // instead of the ~10-instruction division sequence. q0 = RN(a y) is within
 // 1.5 ulp of a/b; one Newton-Markstein correction q1 = RN(q0 + RN(a - b q0) y)
-// (the remainder exact by fma) is faithful; a second one, q2, is then the
-// correctly rounded quotient (Markstein's theorem: y within half an ulp of
-// 1/b and a faithful q). The theorem excludes under/overflow and non-finite
-// a, so q2 is returned with `bad` set when |q2| is outside the exponent range
-// where it is proven (biased exponent 23 ... 2022, i.e. [2^-1000, 2^1000);
-// zero, subnormals, inf and NaN excluded): the caller tests one flag for
-// several quotients and takes the IEEE division in its rare branch (a = 0
-// then keeps its sign).
-template <class T> __device__ __forceinline__ T div_by_const_q(T a, T b, T y, bool& bad) {
+// is faithful; a second one, q2, is then the correctly rounded quotient
+// (Markstein's theorem: y within half an ulp of 1/b and a faithful q). The
+// theorem needs each remainder a - b q exact, which holds while the dividend
+// is at least 2^(emin + p) (f64 2^-969, f32 2^-102; below that the remainder
+// can fall into the subnormal range and round), and excludes under/overflow
+// and non-finite a. So q2 is returned with `bad` set when |q2| is outside the
+// exponent range [lo, hi] where both hold: hi = 2^1000 (f32 2^98), and lo the
+// larger of 2^-1000 (f32 2^-99) and the quotient of the smallest safe
+// dividend, 2^-968 (f32 2^-100), by b -- one per divisor (DivConst), so the
+// test stays one exponent compare per quotient. The caller tests one flag for
+// several quotients and takes the IEEE division in its rare branch (zero,
+// subnormal, inf and NaN quotients are all outside; a = 0 then keeps its sign).
+template <class T> struct DivConst {
+  T b, y;             // the divisor and RN(1 / b)
+  uint32_t lo, span;  // q2's biased exponent must lie in [lo, lo + span]
+  __host__ __device__ static DivConst make(T b) {
+    DivConst d;
+    d.b = b;
+    d.y = (T)1 / b;
+    // eb = floor(log2 b) for a normal b > 0 (else the bound below is moot:
+    // y or q0 is then non-finite and q2 falls out of range by itself)
+    if constexpr (sizeof(T) == 8) {
+      const int eb = (int)((__builtin_bit_cast(uint64_t, b) >> 52) & 0x7FF) - 1023;
+      const int lo = 57 - eb > 23 ? 57 - eb : 23;  // |q2| >= 2^(lo-1023) => |a| >= 2^-968
+      d.lo = lo > 2022 ? 2022u : (uint32_t)lo;
+      d.span = 2022u - d.lo;
+    } else {
+      const int eb = (int)((__builtin_bit_cast(uint32_t, b) >> 23) & 0xFF) - 127;
+      const int lo = 28 - eb > 28 ? 28 - eb : 28;   // |q2| >= 2^(lo-127) => |a| >= 2^-100
+      d.lo = lo > 225 ? 225u : (uint32_t)lo;
+      d.span = 225u - d.lo;
+    }
+    return d;
+  }
+};
+template <class T> __device__ __forceinline__ T div_by_const_q(T a, const DivConst<T>& dc, bool& bad) {
+  const T b = dc.b, y = dc.y;
   const T q0 = a * y;
   const T q1 = gfma(gfma(-b, q0, a), y, q0);
   const T q2 = gfma(gfma(-b, q1, a), y, q1);
   if constexpr (sizeof(T) == 8) {
     const uint32_t ex = (uint32_t)(__builtin_bit_cast(uint64_t, q2) >> 52) & 0x7FFu;
-    bad |= ex - 23u > 1999u;
+    bad |= ex - dc.lo > dc.span;
   } else {
-    const uint32_t ex = (__builtin_bit_cast(uint32_t, q2) >> 23) & 0xFFu;  // [2^-99, 2^99)
-    bad |= ex - 28u > 197u;
+    const uint32_t ex = (__builtin_bit_cast(uint32_t, q2) >> 23) & 0xFFu;
+    bad |= ex - dc.lo > dc.span;
   }
   return q2;
 }
@@ -517,13 +545,14 @@ template <class T> struct IsoGaussT {
   template <int LPC, int E> __device__ __forceinline__ IsoGaussLane<T> bind(int) const;
 };
 template <class T> struct IsoGaussLane {
-  T var, iv;  // std*std and RN(1 / var)
+  T var;
+  DivConst<T> dv;  // std*std, its reciprocal and the fast quotient's range
   int D;
   // g = (-x) / var for the coordinates i0 + e < D, +0 past D
   template <int E> __device__ __forceinline__ void grad(const T (&x)[E], T (&g)[E], int i0) const {
     bool bad = false;
 #pragma unroll
-    for (int e = 0; e < E; ++e) g[e] = (i0 + e < D) ? div_by_const_q(-x[e], var, iv, bad) : (T)0;
+    for (int e = 0; e < E; ++e) g[e] = (i0 + e < D) ? div_by_const_q(-x[e], dv, bad) : (T)0;
     if (__builtin_expect(bad, 0)) {
 #pragma unroll
       for (int e = 0; e < E; ++e)
@@ -542,7 +571,7 @@ template <class T> struct IsoGaussLane {
   }
   __device__ __forceinline__ T quot(T a) const {
     bool bad = false;
-    T q = div_by_const_q(a, var, iv, bad);
+    T q = div_by_const_q(a, dv, bad);
     if (__builtin_expect(bad, 0)) q = a / var;
     return q;
   }
@@ -573,7 +602,7 @@ template <int LPC, int E>
 __device__ __forceinline__ IsoGaussLane<T> IsoGaussT<T>::bind(int) const {
   IsoGaussLane<T> r;
   r.var = var;
-  r.iv = (T)1 / var;
+  r.dv = DivConst<T>::make(var);
   r.D = D;
   return r;
 }

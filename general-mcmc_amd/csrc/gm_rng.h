@@ -451,6 +451,29 @@ __device__ __forceinline__ u32x4 draw_block_v(uint64_t seed, uint32_t chain, uin
   }
   return c;
 }
+// N blocks of consecutive idx0 + n (the same chain, block and tag), rounds
+// outermost: the N independent round chains are issued side by side, so each
+// multiply's latency is covered by the other blocks' (the MH proposal draws
+// of a lane's E coordinates). Each block equals draw_block_v's.
+template <int N>
+__device__ __forceinline__ void draw_blocks_v(u32x4 (&c)[N], uint64_t seed, uint32_t chain, uint64_t blk,
+                                              uint32_t tag, uint32_t idx0) {
+#pragma unroll
+  for (int n = 0; n < N; ++n) c[n] = u32x4{idx0 + (uint32_t)n, chain, (uint32_t)blk, tag | ((uint32_t)(blk >> 32) << 8)};
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const uint64_t p0 = (uint64_t)0xD2511F53u * c[n].x, p1 = (uint64_t)0xCD9E8D57u * c[n].z;
+      const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+      const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
+      c[n] = u32x4{xor3(hi1, c[n].y, k0), lo1, xor3(hi0, c[n].w, k1), lo0};
+    }
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
 #endif
 
 // ---- NUTS per-transition draws (stream spec v3) ----------------------------
@@ -577,6 +600,73 @@ __device__ __forceinline__ double sqrt_unscaled(double x) {
   d = __builtin_fma(-g, g, x);
   g = __builtin_fma(d, h, g);
   return x == 0.0 ? x : g;
+}
+// N pairs side by side, statement by statement (the same operations per
+// pair as normals_tab below, so the same bits): the pairs' dependent f64
+// chains are independent of one another, and issuing them interleaved lets
+// each cover the others' latency.
+template <int N>
+__device__ __forceinline__ void normals_tab_n(const u32x4 (&x)[N], double (&z0)[N], double (&z1)[N], const BmLds& t) {
+  double u1[N], r[N], p[N], lnu[N], rad[N], th[N], zz[N], sth[N], cm[N];
+  gm_bm_d2 lc[N], sc[N];
+  int e[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const double D1 = u2d(((uint64_t)(0x43300000u | (x[n].x >> 12)) << 32) |
+                          (((x[n].x << 20) & 0xFE000000u) | (x[n].y >> 7)));
+    u1[n] = __builtin_fma(D1, 0x1p-52, u2d((x[n].y & 64u) ? 0xBFEFFFFFFFFFFFFEull : 0xBFEFFFFFFFFFFFFFull));
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const uint64_t b = d2u(u1[n]);
+    e[n] = (int)(b >> 52) - 1023;
+    const uint64_t mb = b & 0x000fffffffffffffull;
+    lc[n] = t.lg[(int)(mb >> 45)];
+    sc[n] = t.sc[(int)(x[n].z >> 24)];
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const uint64_t mb = d2u(u1[n]) & 0x000fffffffffffffull;
+    const double m = u2d(mb | 0x3ff0000000000000ull);
+    r[n] = __builtin_fma(m, lc[n].x, -1.0);
+    const double D2 = u2d(((uint64_t)(0x43300000u | ((x[n].z >> 11) & 0x1FFFu)) << 32) |
+                          (((x[n].z << 21) & 0xFC000000u) | (x[n].w >> 6)));
+    th[n] = __builtin_fma(D2, 0x1.921fb54442d18p-51, -0x1.921fb54442d18p+1);
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) p[n] = __builtin_fma(r[n], -0x1.5555555555555p-3, 0x1.999999999999ap-3);
+#pragma unroll
+  for (int n = 0; n < N; ++n) zz[n] = th[n] * th[n];
+#pragma unroll
+  for (int n = 0; n < N; ++n) p[n] = __builtin_fma(r[n], p[n], -0.25);
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    sth[n] = __builtin_fma(th[n] * zz[n], __builtin_fma(zz[n], __builtin_fma(zz[n], -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7),
+                                                        -0x1.5555555555555p-3), th[n]);
+    cm[n] = zz[n] * __builtin_fma(zz[n], __builtin_fma(zz[n], -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5), -0.5);
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) p[n] = __builtin_fma(r[n], p[n], 0x1.5555555555555p-2);
+#pragma unroll
+  for (int n = 0; n < N; ++n) p[n] = __builtin_fma(r[n], p[n], -0.5);
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const double l1 = __builtin_fma(r[n] * r[n], p[n], r[n]);
+    const double de = (double)e[n];
+    lnu[n] = __builtin_fma(de, 0x1.62e42fefa39efp-1, __builtin_fma(de, 0x1.abc9e3b39803fp-56, lc[n].y + l1));
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const double m2l = -2.0 * lnu[n];
+    rad[n] = sqrt_unscaled(m2l > 0.0 ? m2l : 0.0);
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const double sv = __builtin_fma(sc[n].y, sth[n], __builtin_fma(sc[n].x, cm[n], sc[n].x));
+    const double cv = __builtin_fma(-sc[n].x, sth[n], __builtin_fma(sc[n].y, cm[n], sc[n].y));
+    z0[n] = rad[n] * cv;
+    z1[n] = rad[n] * sv;
+  }
 }
 __device__ __forceinline__ void normals_tab(u32x4 x, double (&z)[2], const BmLds& t) {
   // ln u1

@@ -213,6 +213,8 @@ struct gm_sampler {
   void* d_zs = nullptr;  // wide-layout HMC momentum scratch
   size_t zs_bytes = 0;
   Layout lay;
+  bool lay_from_wide = false;  // NUTS: a wide layout replaced for a dense metric (gm_nuts_set_mass_adaptation)
+  Layout lay_wide{};            // ... and that layout
   long long steps_per_launch = 1000;
   int lf_unroll = 0;  // HMC leapfrog-loop unroll: 0 by the wave count (hmc_lf_unroll), else 1, 2 or 4
   std::vector<hipEvent_t> evs;
@@ -657,6 +659,7 @@ int gm_sampler_set_layout(gm_sampler* s, int32_t lanes, int32_t elems) {
          "layout wastes more than half of its lanes");
   s->lay.lanes = lanes;
   s->lay.elems = elems;
+  s->lay_from_wide = false;  // the caller's choice stands
   return GM_OK;
 }
 
@@ -1199,16 +1202,34 @@ int gm_nuts_set_mass_adaptation(gm_sampler* s, int32_t mode, int64_t start_buffe
   GM_HIP(hipStreamSynchronize(s->stream));
   // dense only up to dense_max_dim, else diagonal (generic_nuts.rs:613-620)
   if (mode == 2 && s->D > dense_max_dim) mode = 1;
-  // a dense metric's products broadcast within one wave: off the wide layouts
-  if (mode == 2 && layout_is_wide(s->lay)) s->lay = default_layout(s->D, s->dt, s->tg.kind);
-  return nuts_set_mass(&s->nuts, s->dt, s->C, s->D, mode, start_buffer, end_buffer, initial_window,
-                       regularize, jitter);
+  const int rc = nuts_set_mass(&s->nuts, s->dt, s->C, s->D, mode, start_buffer, end_buffer, initial_window,
+                               regularize, jitter);
+  if (rc != GM_OK) return rc;  // (the layout is left as it was)
+  if (mode == 2 && layout_is_wide(s->lay)) {
+    // a dense metric's products broadcast within one wave: off the wide
+    // layouts, remembered so that a later identity / diagonal mode gets the
+    // wide layout back (the one-wave layouts spill at D > 256)
+    s->lay_wide = s->lay;
+    s->lay = default_layout(s->D, s->dt, s->tg.kind);
+    s->lay_from_wide = true;
+  } else if (mode != 2 && s->lay_from_wide) {
+    s->lay = s->lay_wide;
+    s->lay_from_wide = false;
+  }
+  return GM_OK;
 }
 
 int gm_nuts_set_momentum_pass(gm_sampler* s, int32_t on) {
   GM_REQ(s, "sampler is NULL");
   GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");
   s->nuts.momentum_pass = on != 0;
+  if (!s->nuts.momentum_pass && s->nuts.zbuf) {  // the pass's buffer is released with it
+    GM_HIP(hipSetDevice(s->device));
+    GM_HIP(hipStreamSynchronize(s->stream));
+    GM_HIP(hipFree(s->nuts.zbuf));
+    s->nuts.zbuf = nullptr;
+    s->nuts.zbuf_bytes = 0;
+  }
   return GM_OK;
 }
 
@@ -1234,10 +1255,11 @@ int gm_nuts_set_dense_forms(gm_sampler* s, int32_t minv_lds, int32_t chol_lds) {
   return GM_OK;
 }
 
-int gm_nuts_get_plan(gm_sampler* s, int32_t* plan) {
+int gm_nuts_get_plan(gm_sampler* s, int32_t* plan, int32_t cap) {
   GM_REQ(s && plan, "NULL argument");
   GM_REQ(s->kind == K_NUTS, "not a NUTS sampler");
-  for (int i = 0; i < 6; ++i) plan[i] = s->nuts.plan[i];
+  GM_REQ(cap >= 1, "cap must be >= 1 (the values plan can hold)");
+  for (int i = 0; i < 6 && i < cap; ++i) plan[i] = s->nuts.plan[i];
   return GM_OK;
 }
 

@@ -6,6 +6,10 @@
 #include "gm_launch.h"
 #include "gm_track.h"
 
+#ifndef GM_MH_DRAW_FORM
+#define GM_MH_DRAW_FORM 2
+#endif
+
 namespace gm {
 
 template <class T, int LPC, int E, class TG>
@@ -32,7 +36,7 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   const T sd = (T)a.prop_std;
   const T var = sd * sd;
   const T two_var = (T)2 * var;
-  const T inv_two_var = (T)1 / two_var;  // div_by_const_q: the exact quotient by two_var
+  const DivConst<T> dq = DivConst<T>::make(two_var);  // div_by_const_q: the exact quotient by two_var
   const T pi = (T)3.14159265358979323846;
   const T qconst = (-(T)D * (T)0.5) * glog(((var * pi) * sd) * sd);
 
@@ -65,18 +69,58 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
     // f64: the coordinates' pairs are all fresh at the same steps (the block
     // index is the lane-independent st / 2), one wave-uniform test
     const bool fresh = TAB && (st / 2 != tb);
+#if GM_MH_DRAW_FORM == 1
+    if constexpr (TAB) {
+      // the lane's E pairs drawn in one basic block: their Philox and
+      // Box-Muller chains are independent, so the scheduler interleaves them
+      // and one chain's f64 latency is covered by the others' instructions
+      // (a padded slot's pair is selected to +0, the value it always holds)
+      if (fresh) {
+        u32x4 w[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) w[e] = draw_block_v(a.seed, cid, st / 2, TAG_MH_PROP, (uint32_t)(lane * E + e));
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          double z[2];
+          normals_tab(w[e], z, bm_lds[0]);
+          const bool in = lane * E + e < D;
+          tz0[e] = in ? z[0] : 0.0;
+          tz1[e] = in ? z[1] : 0.0;
+        }
+      }
+    }
+#elif GM_MH_DRAW_FORM == 2
+    if constexpr (TAB) {
+      // the lane's E blocks and pairs issued side by side (draw_blocks_v,
+      // normals_tab_n): independent chains interleaved statement by statement
+      if (fresh) {
+        u32x4 w[E];
+        double z0[E], z1[E];
+        draw_blocks_v<E>(w, a.seed, cid, st / 2, TAG_MH_PROP, (uint32_t)(lane * E));
+        normals_tab_n<E>(w, z0, z1, bm_lds[0]);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const bool in = lane * E + e < D;
+          tz0[e] = in ? z0[e] : 0.0;
+          tz1[e] = in ? z1[e] : 0.0;
+        }
+      }
+    }
+#endif
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
       if constexpr (TAB) {
         // (a padded slot keeps its pair at +0, so its y = +0 + +0 * sd = +0:
         // no branch around the proposal, only around the draw)
+#if GM_MH_DRAW_FORM == 0
         if (fresh && i < D) {
           double z[2];
           normals_tab(draw_block_v(a.seed, cid, st / 2, TAG_MH_PROP, (uint32_t)i), z, bm_lds[0]);
           tz0[e] = z[0];
           tz1[e] = z[1];
         }
+#endif
         y[e] = x[e] + ((st & 1u) ? tz1[e] : tz0[e]) * sd;
       } else {
         y[e] = (i < D) ? x[e] + ncache[e].get(a.seed, cid, st, TAG_MH_PROP, (uint32_t)i) * sd : (T)0;
@@ -86,7 +130,7 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
       // form for every coordinate first (div_by_const_q), one range test for
       // the lane's E quotients, the IEEE division in a branch no wave meets
       // in practice
-      ex[e] = (i < D) ? div_by_const_q(-(d * d), two_var, inv_two_var, qbad) : (T)0;
+      ex[e] = (i < D) ? div_by_const_q(-(d * d), dq, qbad) : (T)0;
     }
     if constexpr (TAB) tb = st / 2;
     if (__builtin_expect(qbad, 0)) {

@@ -643,6 +643,9 @@ constexpr int NPROF_WAVES = 8192;
 __device__ unsigned long long gm_nuts_prof_buf[NPROF_WAVES * NPROF_SLOTS];
 #endif
 
+#ifndef GM_NUTS_UCLIMB
+#define GM_NUTS_UCLIMB 1
+#endif
 // Launch bound: 2 blocks (2 waves per SIMD) per CU, 256 registers per lane,
 // for up to 8 f32 or 2 f64 coordinates per lane (cfg3's 16x2 measured
 // fastest there, profiles/r03/ab/nuts_layouts.jsonl); 1 (512 registers) for
@@ -767,6 +770,21 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       for (int e = 0; e < E; ++e) {
         const int i = lane * E + e;
         out[e] = (i < D) ? sv[i] : (T)0;
+      }
+    }
+  };
+  // the same read for a wave-uniform level k where only some chains use it:
+  // registers and LDS are read by every lane (in bounds, and an LDS read costs
+  // no more for the lanes that discard it), HBM only by the lanes of pred
+  auto stack_vec_if = [&](int k, int f, T (&out)[E], bool pred) __attribute__((always_inline)) {
+    if ((L0REG && k == 0) || k < KL) {
+      stack_vec(k, f, out);
+    } else {
+      const T* sv = svec + ((long long)(k * 3 + f) * C + c) * D;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        out[e] = (pred && i < D) ? sv[i] : (T)0;
       }
     }
   };
@@ -1187,6 +1205,68 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
 #endif
     // climb: merge with the stored left siblings this leaf completes
     bool done = false;
+#if GM_NUTS_UCLIMB
+    // Wave-uniform climb: the level k is one counter for the wave (a scalar),
+    // and each chain's part of trip k is decided by selects. A chain at level
+    // k < j either completes a right child (bit k of its leaf index l is 1:
+    // merge with the stored left sibling and go on up), or is a left child:
+    // stored there if its subtree goes on (ts), else passed up unchanged (a
+    // truncated left subtree's parent builds no right half). At k == j the
+    // doubling is complete. The trips are the wave's longest climb, as in the
+    // per-chain loop, without its exec-mask bookkeeping; the merges and their
+    // draws are each chain's own, in the recursion's post-order.
+    {
+      bool act = true;
+      for (int k = 0;; ++k) {
+        const bool top = act && k == j;
+        done = done || top;
+        act = act && !top;
+        const bool rbit = ((l >> k) & 1) != 0;
+        const bool mrg = act && rbit;
+        const bool sto = act && !rbit && ts;
+        act = act && !sto;
+        if (__builtin_amdgcn_ballot_w64(mrg) != 0) {
+#ifdef GM_NUTS_PROF
+          f_merge = true;
+#endif
+          T lq[E], lpv[E], lpr[E];
+          stack_vec_if(k, 0, lq, mrg);
+          stack_vec_if(k, 1, lpv, mrg);
+          stack_vec_if(k, 2, lpr, mrg);
+          // (values, not places: without this the compiler selects between
+          // the arrays' addresses and keeps both in scratch)
+#pragma unroll
+          for (int e = 0; e < E; ++e) asm volatile("" : "+v"(lq[e]), "+v"(lpv[e]), "+v"(lpr[e]));
+          // the U-turn over the merged subtree's ends: the edge (qe, pe) and
+          // the left sibling's first point (lq, lpv), unordered (no_uturn_ends)
+          const bool nu = no_uturn_ends<LPC, E>(qe, lq, pe, lpv, v);
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            fq[e] = mrg ? lq[e] : fq[e];
+            fp[e] = mrg ? lpv[e] : fp[e];
+          }
+          int ln_, lna;
+          T lal;
+          stack_scalars(k, lal, ln_, lna);
+          const double u = nuts_u<double>(key, 64u + merge_ctr);
+          merge_ctr += mrg ? 1u : 0u;
+          const int den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
+          const bool below = draw_below_ratio(u, (double)tn, (double)den);
+          const bool keep_left = mrg & !below;
+#pragma unroll
+          for (int e = 0; e < E; ++e) pr[e] = keep_left ? lpr[e] : pr[e];
+          tn = mrg ? ln_ + tn : tn;
+          ts = mrg ? (ts && nu) : ts;
+          ta = mrg ? lal + ta : ta;
+          tna = mrg ? lna + tna : tna;
+        }
+        if (__builtin_amdgcn_ballot_w64(sto) != 0) {
+          if (sto) stack_store(k, fq, fp, pr, ta, tn, tna);
+        }
+        if (__builtin_amdgcn_ballot_w64(act) == 0) break;
+      }
+    }
+#else
     int k = 0;
     while (true) {
       if (k == j) { done = true; break; }
@@ -1232,6 +1312,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       for (int e = 0; e < E; ++e) { fq[e] = lq[e]; fp[e] = lpv[e]; }
       ++k;
     }
+#endif
 #ifdef GM_NUTS_PROF
     GM_PSEG(6);
 #endif

@@ -549,8 +549,15 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
           if (ns.zbuf) hipFree(ns.zbuf);
           ns.zbuf = nullptr;
           ns.zbuf_bytes = 0;
-          if (hipMalloc(&ns.zbuf, zb) == hipSuccess) ns.zbuf_bytes = zb;
-          else (void)hipGetLastError();  // no buffer: the kernel draws its momenta
+          // at most a quarter of the device memory free now: the buffer is
+          // kept for the sampler's later launches (gm_nuts_set_momentum_pass(s,
+          // 0) releases it), and must not crowd out other samplers' or the
+          // caller's allocations; without it the kernel draws its momenta
+          size_t fr = 0, tot = 0;
+          if (hipMemGetInfo(&fr, &tot) == hipSuccess && zb <= fr / 4 && hipMalloc(&ns.zbuf, zb) == hipSuccess)
+            ns.zbuf_bytes = zb;
+          else
+            (void)hipGetLastError();
         }
         if (ns.zbuf) {
           const long long S = dt == GM_F32 ? 4 : 2;

@@ -121,7 +121,7 @@ class NUTS(Sampler):
     def launch_plan(self) -> dict:
         """The last launch's on-chip plan (gm_nuts_get_plan)."""
         p = np.zeros(6, dtype=np.int32)
-        _lib.check(self._lib.gm_nuts_get_plan(self._h, _lib.ptr(p)))
+        _lib.check(self._lib.gm_nuts_get_plan(self._h, _lib.ptr(p), len(p)))
         return {"lds_levels": int(p[0]), "minv_lds": int(p[1]), "minv_off": int(p[2]), "chol_lds": int(p[3]),
                 "chol_off": int(p[4]), "frozen": int(p[5])}
 

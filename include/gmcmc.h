@@ -223,7 +223,10 @@ int gm_nuts_get_step_size(gm_sampler* s, double* eps, double* eps_bar);
  * up to 400) the metric becomes (1-regularize)*cov + regularize (diagonal
  * floored at jitter), the step size is re-found from a probe momentum and
  * dual averaging restarts (:897-921, 948-997). Resets the metric to identity
- * and the window schedule to its start; call before the first run. */
+ * and the window schedule to its start; call before the first run. A dense
+ * metric runs on a one-wave layout: once the mode is accepted, a wide layout
+ * (lanes > 64) is replaced by the default one, and restored when a later call
+ * selects mode 0 or 1; on an error the layout is unchanged. */
 int gm_nuts_set_mass_adaptation(gm_sampler* s, int32_t mode, int64_t start_buffer, int64_t end_buffer,
                                 int64_t initial_window, double regularize, double jitter,
                                 int64_t dense_max_dim);
@@ -251,13 +254,16 @@ int gm_nuts_set_dense_forms(gm_sampler* s, int32_t minv_lds, int32_t chol_lds);
  * plan[1] M^-1 form (0 global, 1 packed, 2 full), plan[2] its LDS offset,
  * plan[3] Cholesky factor in LDS (0/1), plan[4] its offset, plan[5] 1 when
  * the launch ran the frozen-dense kernel (every chain's metric dense, no
- * warm-up window: GM_FROZEN_WAVES waves per SIMD). plan holds 6 values. */
-int gm_nuts_get_plan(gm_sampler* s, int32_t* plan);
+ * warm-up window: GM_FROZEN_WAVES waves per SIMD). The first min(cap, 6)
+ * values are written to plan (cap >= 1); returns GM_OK. */
+int gm_nuts_get_plan(gm_sampler* s, int32_t* plan, int32_t cap);
 
 /* Where the NUTS transition momenta are drawn: on (default) in one parallel
- * pass per launch ahead of the tree kernel, into a [steps][C][D] buffer (at
- * most 4 GiB; larger launches draw in the kernel), off in the tree kernel at
- * each transition start. The same Philox/Box-Muller values either way
+ * pass per launch ahead of the tree kernel, into a [steps][C][D] buffer that
+ * the sampler keeps for its later launches (at most 4 GiB and a quarter of
+ * the device memory free when it grows; a launch it does not fit draws in the
+ * kernel), off in the tree kernel at each transition start (switching it off
+ * releases the buffer). The same Philox/Box-Muller values either way
  * (identical results); no reference counterpart. */
 int gm_nuts_set_momentum_pass(gm_sampler* s, int32_t on);
 

@@ -440,6 +440,11 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #define NUTS_U or_nuts_u_d
 #define NUTS_EXP1 nuts_exp1_d
 #define MACH_EPS 2.220446049250313e-16
+/* form 1's elementary functions: the C library's, which the reference's
+ * f64::exp / ln / powf call on Linux (LLVM lowers them to libm) */
+#define REXP exp
+#define RLOG log
+#define RPOW pow
 #include "gm_oracle_t.inc"
 #undef T
 #undef SFX
@@ -455,6 +460,9 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #undef NUTS_U
 #undef NUTS_EXP1
 #undef MACH_EPS
+#undef REXP
+#undef RLOG
+#undef RPOW
 
 #define T float
 #define SFX _f
@@ -470,6 +478,9 @@ static void parallel_chains(int64_t C, int threads, void (*fn)(void*, int64_t, i
 #define NUTS_U or_nuts_u_f
 #define NUTS_EXP1 nuts_exp1_f
 #define MACH_EPS 1.1920928955078125e-07f
+#define REXP expf
+#define RLOG logf
+#define RPOW powf
 #include "gm_oracle_t.inc"
 #undef T
 #undef SFX

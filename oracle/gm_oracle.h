@@ -84,16 +84,32 @@ int or_hmc_run_f(const or_target* t, int lanes, int elems, int64_t C, int D, flo
                  int64_t collect_from, float* samples, int64_t* accepts, int threads, int form);
 
 /* ---- MH: metropolis_hastings.rs:306-318 per chain ---- */
+/* form 0: the kernels' arithmetic (canonical-order sums, the forward and
+ * backward proposal densities one value, the carried log-density); form 1:
+ * the reference's op structure (IsotropicGaussian's proposal and target sums
+ * left to right, distributions.rs:378-406; log q forward and backward
+ * separately and the current log-density recomputed, :306-318) */
 int or_mh_run_d(const or_target* t, int lanes, int elems, int64_t C, int D, double* q,
                 double prop_std, uint64_t seed, uint64_t step0, uint32_t chain_offset,
                 int64_t n_steps, int64_t collect_from, double* samples, int64_t* accepts,
-                int threads);
+                int threads, int form);
 int or_mh_run_f(const or_target* t, int lanes, int elems, int64_t C, int D, float* q,
                 double prop_std, uint64_t seed, uint64_t step0, uint32_t chain_offset,
                 int64_t n_steps, int64_t collect_from, float* samples, int64_t* accepts,
-                int threads);
+                int threads, int form);
+/* one step's terms from states x [C][D] at counter st, in either form: the
+ * log acceptance ratio la, the proposal's log-density lp1, the accept
+ * log-uniform lnu (each [C]); the states are not moved */
+int or_mh_terms_d(const or_target* t, int lanes, int elems, int64_t C, int D, const double* x,
+                  double prop_std, uint64_t seed, uint64_t st, uint32_t chain_offset, int form,
+                  double* la, double* lp1, double* lnu, int threads);
+int or_mh_terms_f(const or_target* t, int lanes, int elems, int64_t C, int D, const float* x,
+                  double prop_std, uint64_t seed, uint64_t st, uint32_t chain_offset, int form,
+                  float* la, float* lp1, float* lnu, int threads);
 
-/* ---- NUTS: generic_nuts.rs:731-1418 per chain (identity mass) ----
+/* ---- NUTS: generic_nuts.rs:731-1418 per chain (identity mass; the
+ * engine's arithmetic -- or_nuts_mass_run with mode 0 and form 1 is the
+ * reference's op structure: left-to-right kinetic sum and U-turn dots) ----
  * state arrays eps/eps_bar/h_bar/mu are [C]; progress selects run_progress
  * semantics; samples [n_collect][C][D]. init_step is the counter value of the
  * init draw; transitions use init_step + 0 .. total-1. */
@@ -129,8 +145,9 @@ typedef struct or_mass_cfg {
   int64_t start_buffer, end_buffer, initial_window;
   double regularize, jitter;
   int form; /* NUTS arithmetic: 0 the engine's (the kernels, bitwise), 1 the reference's op
-             * structure (generic_nuts.rs:227-276, 1357-1418: fresh M^-1 products with two
-             * roundings, left-to-right kinetic sums) */
+             * structure (generic_nuts.rs:227-276, 1343-1418: fresh M^-1 products with two
+             * roundings, left-to-right kinetic sums and U-turn dots; with mode 0 the
+             * identity metric's) */
 } or_mass_cfg;
 typedef struct or_mass_state {
   int32_t* kind;     /* [C]: 0 identity, 1 diagonal, 2 dense */

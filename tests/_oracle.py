@@ -65,7 +65,9 @@ def load():
         getattr(lib, f"or_hmc_run_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _dbl, _int,
                                                       _u64, _u64, _u32, _i64, _i64, _vp, _vp, _int, _int]
         getattr(lib, f"or_mh_run_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _dbl, _u64,
-                                                     _u64, _u32, _i64, _i64, _vp, _vp, _int]
+                                                     _u64, _u32, _i64, _i64, _vp, _vp, _int, _int]
+        getattr(lib, f"or_mh_terms_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _dbl, _u64, _u64,
+                                                       _u32, _int, _vp, _vp, _vp, _int]
         getattr(lib, f"or_nuts_run_{sfx}").argtypes = [tp, _int, _int, _i64, _int, _vp, _vp, _vp,
                                                        _vp, _vp, _dbl, _int, _u64, _u64, _u32,
                                                        _i64, _i64, _int, _vp, _vp, _vp, _int]
@@ -84,6 +86,10 @@ def load():
     lib.or_mass_dense_kat.argtypes = [_vp, _int, _dbl, _vp, _vp]
     lib.or_mass_warmup_diag_kat.argtypes = [_vp, _int, _int, _dbl, _dbl, _vp, _vp]
     lib.or_philox.argtypes = [C.POINTER(C.c_uint32)] * 3
+    lib.or_nuts_key.restype = _u64
+    lib.or_nuts_key.argtypes = [_u64, _u32, _u64, C.POINTER(C.c_uint32)]
+    lib.or_nuts_u_d.restype = _dbl
+    lib.or_nuts_u_d.argtypes = [_u64, _u32]
     lib.or_find_reasonable_epsilon_d.restype = _dbl
     lib.or_find_reasonable_epsilon_d.argtypes = [tp, _int, _int, _vp, _vp]
     lib.or_build_tree_d.argtypes = [tp, _int, _int, _vp, _vp, _vp, _dbl, _int, _int, _dbl, _dbl,
@@ -209,6 +215,12 @@ class Oracle:
         self.lib.or_philox(a, k, o)
         return list(o)
 
+    def nuts_key(self, seed, chain, st):
+        """The NUTS transition's stream key and its Philox words (spec v3)."""
+        w = (C.c_uint32 * 4)()
+        k = self.lib.or_nuts_key(seed, chain, st, w)
+        return k, list(w)
+
     def logp_grad(self, target: Target, x, lanes, elems, dtype):
         x = np.ascontiguousarray(np.atleast_2d(x), dtype=dtype)
         n, d = x.shape
@@ -238,7 +250,10 @@ class Oracle:
         return q, samples, acc
 
     def mh_run(self, target: Target, q, prop_std, seed, step0, n_steps, collect_from, lanes, elems,
-               chain_offset=0, threads=8):
+               chain_offset=0, threads=8, form=0):
+        """form 0: the kernels' arithmetic; 1: the reference's op structure
+        (left-to-right proposal and IsotropicGaussian sums, log q forward and
+        backward separately, metropolis_hastings.rs:306-318)."""
         q = np.array(q, copy=True, order="C")
         C_, D = q.shape
         rows = max(0, n_steps - collect_from)
@@ -247,9 +262,22 @@ class Oracle:
         t = target.struct()
         rc = getattr(self.lib, f"or_mh_run_{_sfx(q.dtype)}")(
             C.byref(t), lanes, elems, C_, D, _p(q), prop_std, seed, step0, chain_offset, n_steps,
-            collect_from, _p(samples), _p(acc), threads)
+            collect_from, _p(samples), _p(acc), threads, form)
         assert rc == 0
         return q, samples, acc
+
+    def mh_terms(self, target: Target, x, prop_std, seed, st, lanes, elems, form, chain_offset=0, threads=8):
+        """One MH step's (log alpha, proposal log-density, ln u) per chain from
+        the states x [C, D] at counter step st, in the given form."""
+        x = np.ascontiguousarray(x)
+        C_, D = x.shape
+        la, lp1, lnu = (np.empty(C_, dtype=x.dtype) for _ in range(3))
+        t = target.struct()
+        rc = getattr(self.lib, f"or_mh_terms_{_sfx(x.dtype)}")(
+            C.byref(t), lanes, elems, C_, D, _p(x), prop_std, seed, st, chain_offset, form, _p(la), _p(lp1),
+            _p(lnu), threads)
+        assert rc == 0
+        return la, lp1, lnu
 
     def nuts_state(self, n, dtype):
         return {"eps": np.full(n, -1.0, dtype=dtype), "eps_bar": np.ones(n, dtype=dtype),
@@ -257,7 +285,14 @@ class Oracle:
                 "mu": np.full(n, np.log(10.0), dtype=dtype)}
 
     def nuts_run(self, target: Target, q, state, target_accept, max_depth, seed, init_step,
-                 n_collect, n_discard, progress, lanes, elems, chain_offset=0, threads=8):
+                 n_collect, n_discard, progress, lanes, elems, chain_offset=0, threads=8, form=0):
+        """form 0: the kernels' arithmetic; 1: the reference's op structure
+        under the identity metric (left-to-right kinetic sum and U-turn dots,
+        generic_nuts.rs:230-235, 1369-1377): or_nuts_mass_run with mode 0."""
+        if form:
+            m = self.nuts_mass(0, np.asarray(q).shape[0], np.asarray(q).shape[1], np.asarray(q).dtype, form=form)
+            return self.nuts_mass_run(target, q, state, m, target_accept, max_depth, seed, init_step, n_collect,
+                                      n_discard, progress, lanes, elems, chain_offset, threads)
         q = np.array(q, copy=True, order="C")
         C_, D = q.shape
         samples = np.zeros((n_collect, C_, D), dtype=q.dtype)

@@ -170,6 +170,42 @@ def test_mh_exact_quotient_edges_bitwise(gm, oracle, dtype, std):
         s.close()
 
 
+@pytest.mark.parametrize("dtype,std", [(np.float32, 1e-16), (np.float64, 1e-150)])
+@pytest.mark.parametrize("lay", [(32, 1), (16, 2), (8, 4)])
+def test_isogauss_target_tiny_std_bitwise(gm, oracle, dtype, std, lay):
+    """An IsotropicGaussian target so narrow that the log-density's dividend
+    -0.5 sum x^2 falls below the fast quotient's safe range (f32 ~2^-102 <
+    2^-100, f64 ~2^-993 < 2^-968; div_by_const_q's per-divisor bound, where
+    the remainder a - b q could round in the subnormal range): HMC, NUTS and
+    MH equal the oracle's IEEE divisions bit for bit."""
+    dim, n_chains = 32, 12
+    x0 = (start(gm, n_chains, dim, np.float64, 1.0) * std).astype(dtype)
+    t = gm.IsotropicGaussian(std)
+    ot = Target.from_product(t, dim)
+    h = gm.HMC(t, x0, 0.2 * std, 5, dtype=dtype).set_seed(4)
+    h.set_layout(*lay)
+    out = h.run(4, 2)
+    _, smp, acc = oracle.hmc_run(ot, x0, 0.2 * std, 5, 4, 0, 6, 2, *lay)
+    np.testing.assert_array_equal(out, smp.transpose(1, 0, 2))
+    np.testing.assert_array_equal(h.accept_counts(), acc)
+    assert 0 < acc.sum()
+    n = gm.NUTS(t, x0, 0.8, dtype=dtype, max_depth=6).set_seed(5)
+    n.set_layout(*lay)
+    out = n.run(4, 3)
+    st = oracle.nuts_state(n_chains, dtype)
+    _, smp, acc, nlf = oracle.nuts_run(ot, x0, st, 0.8, 6, 5, 0, 4, 3, False, *lay)
+    np.testing.assert_array_equal(out, smp.transpose(1, 0, 2))
+    np.testing.assert_array_equal(n.leapfrog_counts(), nlf)
+    eps, _ = n.step_sizes()
+    np.testing.assert_array_equal(eps.astype(dtype), st["eps"])
+    m = gm.MetropolisHastings(t, gm.IsotropicGaussian(0.7 * std), x0, dtype=dtype).seed(6)
+    m.set_layout(*lay)
+    out = m.run(5, 2)
+    _, smp, acc = oracle.mh_run(ot, x0, 0.7 * std, 6, 0, 7, 2, *lay)
+    np.testing.assert_array_equal(out, smp.transpose(1, 0, 2).astype(np.float64))
+    np.testing.assert_array_equal(m.accept_counts(), acc)
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("dim,lay", [(2, (2, 1)), (5, (8, 1)), (32, (32, 1)), (32, (16, 2))])
 @pytest.mark.parametrize("progress", [False, True])
