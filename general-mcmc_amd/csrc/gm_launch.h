@@ -56,6 +56,13 @@ struct MhLaunch {
 };
 
 // ---- NUTS ------------------------------------------------------------------
+// bytes of one HBM subtree-stack entry: three D-vectors, alpha, n, n_alpha,
+// padded to whole 128-byte cache lines
+inline long long nuts_stack_entry_bytes(int D, int tsz) {
+  const long long b = 3LL * D * tsz + tsz + 8;
+  return (b + 127) / 128 * 128;
+}
+
 struct NutsLaunch {
   void* q = nullptr;
   long long* accepts = nullptr;
@@ -65,10 +72,8 @@ struct NutsLaunch {
   void* eps_bar = nullptr;
   void* h_bar = nullptr;
   void* mu = nullptr;
-  void* stk_vec = nullptr;
-  void* stk_alpha = nullptr;
-  int* stk_n = nullptr;
-  int* stk_na = nullptr;
+  void* stk_vec = nullptr;   // HBM stack levels: [C][max_depth] entries of stk_es bytes (gm_nuts.h)
+  long long stk_es = 0;
   long long C = 0;
   int D = 0;
   int max_depth = 10;

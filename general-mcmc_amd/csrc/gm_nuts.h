@@ -17,10 +17,12 @@ struct NutsState {
   void* eps_bar = nullptr;  // [C] T   (:581)
   void* h_bar = nullptr;    // [C] T   (:582)
   void* mu = nullptr;       // [C] T   (:580)
-  void* stk_vec = nullptr;  // [max_depth][3][C][D] T : left-subtree first q, first p, proposal q
-  void* stk_alpha = nullptr;  // [max_depth][C] T  (levels held in HBM)
-  int* stk_n = nullptr;       // [max_depth][C]
-  int* stk_na = nullptr;      // [max_depth][C]
+  // subtree-stack levels held in HBM: per chain max_depth entries of
+  // stk_es bytes, entry = [3][D] T (left-subtree first q, first p, proposal
+  // q), then alpha (T), n, n_alpha (int); one contiguous stretch per (chain,
+  // level) (nuts_stack_entry_bytes)
+  void* stk_vec = nullptr;
+  long long stk_es = 0;
   long long lds_levels_cap = -1;  // subtree-stack levels in LDS: -1 as many as fit
   int dense_minv_lds = 1;     // dense M^-1 in LDS: 1 packed (the default: room for 6 stack levels),
                               // 2 full when it fits (else packed), 0 off

@@ -6,10 +6,6 @@
 #include "gm_launch.h"
 #include "gm_track.h"
 
-#ifndef GM_MH_DRAW_FORM
-#define GM_MH_DRAW_FORM 2
-#endif
-
 namespace gm {
 
 template <class T, int LPC, int E, class TG>
@@ -69,30 +65,12 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
     // f64: the coordinates' pairs are all fresh at the same steps (the block
     // index is the lane-independent st / 2), one wave-uniform test
     const bool fresh = TAB && (st / 2 != tb);
-#if GM_MH_DRAW_FORM == 1
-    if constexpr (TAB) {
-      // the lane's E pairs drawn in one basic block: their Philox and
-      // Box-Muller chains are independent, so the scheduler interleaves them
-      // and one chain's f64 latency is covered by the others' instructions
-      // (a padded slot's pair is selected to +0, the value it always holds)
-      if (fresh) {
-        u32x4 w[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) w[e] = draw_block_v(a.seed, cid, st / 2, TAG_MH_PROP, (uint32_t)(lane * E + e));
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          double z[2];
-          normals_tab(w[e], z, bm_lds[0]);
-          const bool in = lane * E + e < D;
-          tz0[e] = in ? z[0] : 0.0;
-          tz1[e] = in ? z[1] : 0.0;
-        }
-      }
-    }
-#elif GM_MH_DRAW_FORM == 2
     if constexpr (TAB) {
       // the lane's E blocks and pairs issued side by side (draw_blocks_v,
-      // normals_tab_n): independent chains interleaved statement by statement
+      // normals_tab_n): the E coordinates' Philox and Box-Muller chains are
+      // independent, so one chain's f64 latency is covered by the others'
+      // instructions (1.414e9 -> 1.432e9 chain-steps/s against drawing each
+      // coordinate's pair in its own branch, profiles/r06/ab_mh_draw_forms.log)
       if (fresh) {
         u32x4 w[E];
         double z0[E], z1[E];
@@ -106,21 +84,12 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
         }
       }
     }
-#endif
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int i = lane * E + e;
       if constexpr (TAB) {
         // (a padded slot keeps its pair at +0, so its y = +0 + +0 * sd = +0:
         // no branch around the proposal, only around the draw)
-#if GM_MH_DRAW_FORM == 0
-        if (fresh && i < D) {
-          double z[2];
-          normals_tab(draw_block_v(a.seed, cid, st / 2, TAG_MH_PROP, (uint32_t)i), z, bm_lds[0]);
-          tz0[e] = z[0];
-          tz1[e] = z[1];
-        }
-#endif
         y[e] = x[e] + ((st & 1u) ? tz1[e] : tz0[e]) * sd;
       } else {
         y[e] = (i < D) ? x[e] + ncache[e].get(a.seed, cid, st, TAG_MH_PROP, (uint32_t)i) * sd : (T)0;

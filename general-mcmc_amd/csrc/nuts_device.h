@@ -643,9 +643,6 @@ constexpr int NPROF_WAVES = 8192;
 __device__ unsigned long long gm_nuts_prof_buf[NPROF_WAVES * NPROF_SLOTS];
 #endif
 
-#ifndef GM_NUTS_UCLIMB
-#define GM_NUTS_UCLIMB 1
-#endif
 // Launch bound: 2 blocks (2 waves per SIMD) per CU, 256 registers per lane,
 // for up to 8 f32 or 2 f64 coordinates per lane (cfg3's 16x2 measured
 // fastest there, profiles/r03/ab/nuts_layouts.jsonl); 1 (512 registers) for
@@ -679,13 +676,16 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long C = a.C;
   const uint32_t cid = a.chain_offset + (uint32_t)c;
   T* __restrict__ qs = (T*)a.q;
-  T* __restrict__ svec = (T*)a.stk_vec;
-  T* __restrict__ salpha = (T*)a.stk_alpha;
   // Subtree stack. Level k < KL: LDS, vectors [k][field][thread*E + e] of
   // this block, scalars [k][chain in block] (every lane of a chain writes the
   // same value); a lane reads back only what it or its group wrote, so no
-  // synchronisation. Deeper levels: HBM, vectors [k][field][chain][coord],
-  // scalars [k][chain].
+  // synchronisation. Deeper levels: HBM, one entry of a.stk_es bytes per
+  // (chain, level), the chain's entries contiguous: vectors [field][coord],
+  // then alpha, n, n_alpha: a merge's reads are one stretch of cache lines
+  // (the scalars in three [level][chain] arrays cost three more lines per
+  // merge: the frozen-dense kernel, whose levels >= 1 are all in HBM, +5 %,
+  // profiles/r06/ab_nuts_stack_slab.log).
+  char* __restrict__ sbase = (char*)a.stk_vec + c * (long long)a.max_depth * a.stk_es;
   // threads per block (nuts_part.inc): 256, or one chain's LPC > 64
   constexpr int NT = LPC > 64 ? LPC : 256;
   constexpr int CPB = NT / LPC;
@@ -740,19 +740,20 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       lnn[k * CPB + cib] = nn;
       lnna[k * CPB + cib] = nna;
     } else {
-      T* sv = svec + ((long long)(k * 3) * C + c) * D;
+      T* sv = (T*)(sbase + k * a.stk_es);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int i = lane * E + e;
         if (i < D) {
           sv[i] = f0[e];
-          sv[C * D + i] = f1[e];
-          sv[2 * C * D + i] = f2[e];
+          sv[D + i] = f1[e];
+          sv[2 * D + i] = f2[e];
         }
       }
-      salpha[k * C + c] = al;
-      a.stk_n[k * C + c] = nn;
-      a.stk_na[k * C + c] = nna;
+      sv[3 * D] = al;
+      int* sn = (int*)(sv + 3 * D + 1);
+      sn[0] = nn;
+      sn[1] = nna;
     }
   };
   // field f (0 first q, 1 first p, 2 proposal) of level k
@@ -765,7 +766,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
 #pragma unroll
       for (int e = 0; e < E; ++e) out[e] = v[e];
     } else {
-      const T* sv = svec + ((long long)(k * 3 + f) * C + c) * D;
+      const T* sv = (const T*)(sbase + k * a.stk_es) + f * D;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int i = lane * E + e;
@@ -780,7 +781,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     if ((L0REG && k == 0) || k < KL) {
       stack_vec(k, f, out);
     } else {
-      const T* sv = svec + ((long long)(k * 3 + f) * C + c) * D;
+      const T* sv = (const T*)(sbase + k * a.stk_es) + f * D;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int i = lane * E + e;
@@ -798,9 +799,11 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       nn = lnn[k * CPB + cib];
       nna = lnna[k * CPB + cib];
     } else {
-      al = salpha[k * C + c];
-      nn = a.stk_n[k * C + c];
-      nna = a.stk_na[k * C + c];
+      const T* sv = (const T*)(sbase + k * a.stk_es) + 3 * D;
+      al = sv[0];
+      const int* sn = (const int*)(sv + 1);
+      nn = sn[0];
+      nna = sn[1];
     }
   };
 
@@ -1205,7 +1208,6 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
 #endif
     // climb: merge with the stored left siblings this leaf completes
     bool done = false;
-#if GM_NUTS_UCLIMB
     // Wave-uniform climb: the level k is one counter for the wave (a scalar),
     // and each chain's part of trip k is decided by selects. A chain at level
     // k < j either completes a right child (bit k of its leaf index l is 1:
@@ -1266,53 +1268,6 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
         if (__builtin_amdgcn_ballot_w64(act) == 0) break;
       }
     }
-#else
-    int k = 0;
-    while (true) {
-      if (k == j) { done = true; break; }
-      if (((l >> k) & 1) == 0) {  // left child at level k
-        // A truncated left subtree: its parent builds no right half and
-        // returns it unchanged; going up, it is merged wherever that parent
-        // is itself a right child (the recursion's post-order).
-        if (!ts) { ++k; continue; }
-        stack_store(k, fq, fp, pr, ta, tn, tna);
-        break;
-      }
-      // right child: merge with the stored left sibling (:1251-1323)
-#ifdef GM_NUTS_PROF
-      f_merge = true;
-#endif
-      T lq[E], lpv[E];
-      stack_vec(k, 0, lq);
-      stack_vec(k, 1, lpv);
-      int ln_, lna;
-      T lal;
-      stack_scalars(k, lal, ln_, lna);
-      const double u = nuts_u<double>(key, 64u + merge_ctr++);
-      const int den = (ln_ + tn) > 1 ? (ln_ + tn) : 1;
-      // (selects rather than branches from here on: the chains of a wave
-      // take different sides, and a divergent branch costs both)
-      {
-        const bool keep_left = !draw_below_ratio(u, (double)tn, (double)den);
-        T lpr[E];
-        stack_vec(k, 2, lpr);
-#pragma unroll
-        for (int e = 0; e < E; ++e) pr[e] = keep_left ? lpr[e] : pr[e];
-      }
-      tn = ln_ + tn;
-      {
-        // U-turn over the merged subtree's ends: the edge (qe, pe) and the
-        // left sibling's first point (lq, lpv), unordered (no_uturn_ends)
-        const bool nu = no_uturn_ends<LPC, E>(qe, lq, pe, lpv, v);
-        ts = ts && nu;
-      }
-      ta = lal + ta;
-      tna = lna + tna;
-#pragma unroll
-      for (int e = 0; e < E; ++e) { fq[e] = lq[e]; fp[e] = lpv[e]; }
-      ++k;
-    }
-#endif
 #ifdef GM_NUTS_PROF
     GM_PSEG(6);
 #endif

@@ -220,12 +220,8 @@ int nuts_init_state(NutsState* ns, gm_dtype dt, long long C, int D, int max_dept
   if (e == hipSuccess) e = hipMalloc(&ns->h_bar, C * esz);
   if (e == hipSuccess) e = hipMalloc(&ns->mu, C * esz);
   if (e == hipSuccess) e = hipMalloc((void**)&ns->n_leapfrog, C * sizeof(long long));
-  if (e == hipSuccess && max_depth > 0)
-    e = hipMalloc(&ns->stk_vec, (size_t)max_depth * 3 * C * D * esz);
-  // per-chain scalars of the HBM stack levels: [max_depth][C]
-  if (e == hipSuccess && max_depth > 0) e = hipMalloc(&ns->stk_alpha, (size_t)max_depth * C * esz);
-  if (e == hipSuccess && max_depth > 0) e = hipMalloc((void**)&ns->stk_n, (size_t)max_depth * C * sizeof(int));
-  if (e == hipSuccess && max_depth > 0) e = hipMalloc((void**)&ns->stk_na, (size_t)max_depth * C * sizeof(int));
+  ns->stk_es = nuts_stack_entry_bytes(D, (int)esz);
+  if (e == hipSuccess && max_depth > 0) e = hipMalloc(&ns->stk_vec, (size_t)C * max_depth * ns->stk_es);
   if (e != hipSuccess) {
     set_error(std::string("NUTS state allocation failed: ") + hipGetErrorString(e));
     return GM_ENOMEM;
@@ -342,9 +338,6 @@ void nuts_free_state(NutsState* ns) {
   ffree(ns->h_bar);
   ffree(ns->mu);
   ffree(ns->stk_vec);
-  ffree(ns->stk_alpha);
-  ffree(ns->stk_n);
-  ffree(ns->stk_na);
   ffree(ns->n_leapfrog);
   ffree(ns->zbuf);
   *ns = NutsState();
@@ -475,9 +468,7 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     a.h_bar = ns.h_bar;
     a.mu = ns.mu;
     a.stk_vec = ns.stk_vec;
-    a.stk_alpha = ns.stk_alpha;
-    a.stk_n = ns.stk_n;
-    a.stk_na = ns.stk_na;
+    a.stk_es = ns.stk_es;
     a.C = C;
     a.D = D;
     a.max_depth = ns.max_depth;

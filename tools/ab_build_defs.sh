@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B variant: the whole libgmcmc.so built from the WORKING TREE's sources
 # under extra defines, into abtest/NAME (its own build directory):
-#   tools/ab_build_defs.sh NAME "-DGM_NUTS_UCLIMB=0"
+#   tools/ab_build_defs.sh NAME "-DGM_PACKED_BATCH=4"
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; defs=$2
