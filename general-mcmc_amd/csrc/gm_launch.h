@@ -128,6 +128,13 @@ struct NutsLaunch {
   // (nuts_momenta_kernel: the same Philox/Box-Muller values the kernel would
   // draw), or null: drawn in the kernel
   const void* zmom = nullptr;
+  // with zmom, each transition's start record from the same pass
+  // (nuts_starts_kernel, [n_steps][C] each): the stream key K of the
+  // TAG_NUTS_EXP block, ln of its Exp1 uniform, and the doublings' direction
+  // bits (bit j: u(K, 2j) < 1/2) -- the values the kernel would compute
+  const uint64_t* zkey = nullptr;
+  const void* zlnu = nullptr;
+  const uint32_t* zdir = nullptr;
 };
 
 // waves per SIMD of the NUTS dense-metric instantiations (their launch

@@ -586,6 +586,59 @@ __device__ __forceinline__ void bm_lds_fill(BmLds& t) {
     t.sc[k] = gm_bm_d2{gm_bm_sincos[2 * k], gm_bm_sincos[2 * k + 1]};
   }
 }
+// ---- the NUTS leaf's acceptance statistic, f64 (leaf_alpha_tab) -----------
+// min(1, exp(x)) (generic_nuts.rs:1212; Rust's f64::min gives 1 for a NaN) as
+// exp(max(min(x, 0), -746)): a NaN or positive x yields exp(+-0) = 1 exactly,
+// and below -746 the power underflows to +0 as exp's does. The exp is
+// table-driven and division-free (msun's gexp ends in a quotient whose
+// reciprocal and corrections sat on every leaf's critical path):
+//   k = rint(64 x / ln2), r = x - k ln2/64 by two fmas (msun's split of ln2,
+//   scaled by 1/64: k times the high part is exact), |r| <= ln2/128;
+//   exp(r) - 1 = r + r^2 (1/2 + r/6 + ... + r^4/720) (truncation < 3e-20);
+//   exp(x) = ldexp(fma(t, p, t), k >> 6), t = 2^((k & 63)/64) from the table
+//   (gm_bm_tables.h GM_EXP64_INIT, staged in LDS).
+// Within about 1 ulp of exp; oracle/gm_oracle.c or_leaf_alpha_d restates it
+// operation for operation.
+static __constant__ double gm_exp64[64] = {GM_EXP64_INIT};
+__device__ __forceinline__ void exp64_lds_fill(double* t) {
+  for (int k = threadIdx.x; k < 64; k += blockDim.x) t[k] = gm_exp64[k];
+}
+// Its 8 constants live in VGPRs from before the sampler's loop (make()): as
+// SGPR pairs the compiler rebuilt them per use beside the kernel's spilled
+// scalars. Measured against the msun form (profiles/r06/ab_nuts_leaf_exp.log,
+// alternating processes): cfg3 3.59e9 -> 3.77e9 (constants left to the
+// compiler) -> 3.87e9 leapfrogs/s (pinned), dense metric 1.14e9 -> 1.21e9 ->
+// 1.24e9; bitwise against the oracle (434 GPU tests).
+#ifndef GM_LEAF_EXP_PIN
+#define GM_LEAF_EXP_PIN 1
+#endif
+struct LeafExpK {
+  double c[8] = {-746.0, 0x1.71547652b82fep+6, 0x1.62e42fee00000p-7, 0x1.a39ef35793c76p-39,
+                 0x1.6c16c16c16c17p-10, 0x1.1111111111111p-7, 0x1.5555555555555p-5, 0x1.5555555555555p-3};
+  __device__ static LeafExpK make() {
+    LeafExpK K;
+    if (GM_LEAF_EXP_PIN) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(K.c[i]));
+    }
+    return K;
+  }
+};
+__device__ __forceinline__ double leaf_alpha_tab(double x, const double* t, const LeafExpK& K) {
+  const double (&c)[8] = K.c;
+  const double xs = __builtin_fmax(__builtin_fmin(x, 0.0), c[0]);
+  const double dk = __builtin_rint(xs * c[1]);
+  const int k = (int)dk;
+  double r = __builtin_fma(-dk, c[2], xs);
+  r = __builtin_fma(-dk, c[3], r);
+  double a = __builtin_fma(r, c[4], c[5]);
+  a = __builtin_fma(r, a, c[6]);
+  a = __builtin_fma(r, a, c[7]);
+  a = __builtin_fma(r, a, 0.5);
+  const double p = __builtin_fma(r * r, a, r);
+  const double tv = t[k & 63];
+  return __builtin_ldexp(__builtin_fma(tv, p, tv), k >> 6);
+}
 // sqrt(x) for x = 0 or 2^-767 <= x < inf: LLVM's gfx950 f64 sequence (rsq, a
 // Goldschmidt step, two Newton corrections) without its small-input scaling,
 // which is the identity on that range; the same bits as gsqrt there.

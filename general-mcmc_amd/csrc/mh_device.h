@@ -35,6 +35,16 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   const DivConst<T> dq = DivConst<T>::make(two_var);  // div_by_const_q: the exact quotient by two_var
   const T pi = (T)3.14159265358979323846;
   const T qconst = (-(T)D * (T)0.5) * glog(((var * pi) * sd) * sd);
+  // log alpha = (lp' + log q_b) - (lp + log q_f) (metropolis_hastings.rs:312)
+  // with log q_b = log q_f = L, the same bits ((-d)^2 = d^2). Whenever L is
+  // finite -- 2 var a normal number and the constant finite, so that every
+  // d^2 / (2 var) is (|d| < 1e154) -- the engine takes lp' - lp: the same
+  // value up to the rounding of the two sums with L (form 0 of the oracle;
+  // tied to the reference text by tests/test_gpu_forms.py at cfg5's shape),
+  // without the per-coordinate quotients and their reduction. Otherwise
+  // (e.g. var = 0, where the reference's 0/0 rejects every proposal) the
+  // full form.
+  const bool cancel = __builtin_isnormal(two_var) && __builtin_isfinite(qconst);
 
   T x[E], y[E], gdummy[E];
 #pragma unroll
@@ -94,34 +104,46 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
       } else {
         y[e] = (i < D) ? x[e] + ncache[e].get(a.seed, cid, st, TAG_MH_PROP, (uint32_t)i) * sd : (T)0;
       }
-      const T d = y[e] - x[e];
-      // -(d*d) / two_var (distributions.rs:385), the IEEE quotient: its fast
-      // form for every coordinate first (div_by_const_q), one range test for
-      // the lane's E quotients, the IEEE division in a branch no wave meets
-      // in practice
-      ex[e] = (i < D) ? div_by_const_q(-(d * d), dq, qbad) : (T)0;
     }
     if constexpr (TAB) tb = st / 2;
-    if (__builtin_expect(qbad, 0)) {
+    T lp1, log_alpha;
+    if (cancel) {
+      // the symmetric proposal's log q terms cancel (see above): the target's
+      // sum alone
+      lp1 = tg.finish(group_sum<LPC>(tg.template eval_part<LPC, E>(y, gdummy, lane)));
+      log_alpha = lp1 - lp;
+    } else {
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int i = lane * E + e;
         const T d = y[e] - x[e];
-        if (i < D) ex[e] = -(d * d) / two_var;
+        // -(d*d) / two_var (distributions.rs:385), the IEEE quotient: its fast
+        // form for every coordinate first (div_by_const_q), one range test for
+        // the lane's E quotients, the IEEE division in a branch no wave meets
+        // in practice
+        ex[e] = (i < D) ? div_by_const_q(-(d * d), dq, qbad) : (T)0;
       }
-    }
+      if (__builtin_expect(qbad, 0)) {
 #pragma unroll
-    for (int e = 0; e < E; ++e) qpart = (e == 0) ? ex[e] : qpart + ex[e];
-    // the proposal density's sum and the target's, reduced together: the
-    // same stages (and bits) as two group_sums, each stage's DPP latency
-    // covered by the other sum instead of wait states
-    T sums[2];
-    sums[0] = qpart;
-    sums[1] = tg.template eval_part<LPC, E>(y, gdummy, lane);
-    group_sum_n<LPC>(sums);
-    const T logq = sums[0] + qconst;
-    const T lp1 = tg.finish(sums[1]);
-    const T log_alpha = (lp1 + logq) - (lp + logq);
+        for (int e = 0; e < E; ++e) {
+          const int i = lane * E + e;
+          const T d = y[e] - x[e];
+          if (i < D) ex[e] = -(d * d) / two_var;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) qpart = (e == 0) ? ex[e] : qpart + ex[e];
+      // the proposal density's sum and the target's, reduced together: the
+      // same stages (and bits) as two group_sums, each stage's DPP latency
+      // covered by the other sum instead of wait states
+      T sums[2];
+      sums[0] = qpart;
+      sums[1] = tg.template eval_part<LPC, E>(y, gdummy, lane);
+      group_sum_n<LPC>(sums);
+      const T logq = sums[0] + qconst;
+      lp1 = tg.finish(sums[1]);
+      log_alpha = (lp1 + logq) - (lp + logq);
+    }
     T lnu;
     if constexpr (LPC == 64) {
       // the accept log-uniforms of 64 consecutive steps in one VALU pass:

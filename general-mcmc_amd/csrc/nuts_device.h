@@ -670,6 +670,14 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long c = gtid / LPC;
   const int lane = (int)(gtid % LPC);
+  // f64: the leaf's exp table (leaf_alpha_tab), 512 B of static LDS inside
+  // the 1 KiB per block that nuts_size_lds leaves beside the dynamic plan;
+  // filled by the whole block before any thread returns
+  __shared__ double exp_lds[sizeof(T) == 8 ? 64 : 1];
+  if constexpr (sizeof(T) == 8) {
+    exp64_lds_fill(exp_lds);
+    __syncthreads();
+  }
   const auto tg = tg_.template bind<LPC, E>(lane);  // per-lane target view
   if (c >= a.C) return;
   const int D = a.D;
@@ -963,6 +971,10 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   int l = 0, n = 1;
   T joint0 = (T)0, logu = (T)0;
   uint64_t key = 0;
+  uint32_t dirb = 0;  // the transition's direction bits (pre-pass record)
+#ifndef GM_SREC_DENSE
+#define GM_SREC_DENSE 1  // the frozen-dense kernel reads the start records too
+#endif
   uint32_t merge_ctr = 0;
   T fq[E], fp[E], pr[E];  // current subtree: first q, first p, proposal
   int tn = 0, tna = 0;
@@ -996,15 +1008,9 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   // pending at the loop entry, the wait the compiler puts at the loop head
   // would also wait out the previous transition's sample stores.
   __builtin_amdgcn_s_waitcnt(0);
-  const ExpConsts ek = [] {  // the leaf's f64 exp, constants in VGPRs
-    // (not in the frozen-dense kernel: at its 2 waves per SIMD the 20
-    // registers are worth more than the scalar operands they save)
-#ifndef GM_FROZEN_PIN_EXP
-#define GM_FROZEN_PIN_EXP 0
-#endif
-    if constexpr (sizeof(T) == 8 && (MASS != 3 || GM_FROZEN_PIN_EXP)) return ExpConsts::pinned();
-    else return ExpConsts{};
-  }();
+  const LeafExpK lek = LeafExpK::make();  // the leaf exp's constants (f64)
+  // the launch's start records from the momentum pre-pass (a.zkey ...)
+  const bool srec = (GM_SREC_DENSE || MASS != 3) && a.zmom != nullptr;
   while (true) {
     const bool live = s < a.n_steps;
 #ifdef GM_NUTS_PROF
@@ -1051,6 +1057,11 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     // launch's pre-drawn block (their loads in flight under the evaluation
     // below), else drawn here; the metric's product after the evaluation
     T zs[E];
+    // with the pre-pass: the transition's start record as well (its key, the
+    // slice variable's log and the direction bits), loaded with the momenta
+    uint64_t skey = 0;
+    T slnu = (T)0;
+    uint32_t sdir = 0;
     if (live && starting) {
       if (a.zmom != nullptr) {
         const T* __restrict__ zm = (const T*)a.zmom + ((long long)s * C + c) * D;
@@ -1058,6 +1069,11 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
         for (int e = 0; e < E; ++e) {
           const int i = lane * E + e;
           zs[e] = (i < D) ? zm[i] : (T)0;
+        }
+        if (srec) {
+          skey = a.zkey[(long long)s * C + c];
+          slnu = ((const T*)a.zlnu)[(long long)s * C + c];
+          sdir = a.zdir[(long long)s * C + c];
         }
       } else {
 #pragma unroll
@@ -1160,13 +1176,19 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
 #endif
       // --- transition start: slice variable, trajectory ends (:764-781)
       joint0 = lp - kin;
-      const u32x4 kw = draw_block_s(a.seed, cid, st, TAG_NUTS_EXP, 0u);
-      key = nuts_key(kw);
-      // (the table-driven Box-Muller of spec v5 for these momenta and this
-      // Exp1 draw measured -4 % at cfg3, profiles/r04/ab_nuts_tab_momenta.log:
-      // its 6 KiB of LDS tables and ~10 registers cost more than its
-      // instructions save)
-      logu = joint0 + glog_pos(Unif<T>::oc(kw.z, kw.w));  // joint - Exp1
+      if (srec) {  // the pre-pass's record (nuts_starts_kernel): the same values
+        key = skey;
+        logu = joint0 + slnu;
+        dirb = sdir;
+      } else {
+        const u32x4 kw = draw_block_s(a.seed, cid, st, TAG_NUTS_EXP, 0u);
+        key = nuts_key(kw);
+        // (the table-driven Box-Muller of spec v5 for these momenta and this
+        // Exp1 draw measured -4 % at cfg3, profiles/r04/ab_nuts_tab_momenta.log:
+        // its 6 KiB of LDS tables and ~10 registers cost more than its
+        // instructions save)
+        logu = joint0 + glog_pos(Unif<T>::oc(kw.z, kw.w));  // joint - Exp1
+      }
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         qe[e] = q[e]; pe[e] = p0[e]; ge[e] = gx[e];
@@ -1183,7 +1205,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       j = 0;
       l = 0;
       merge_ctr = 0;
-      v = (nuts_u<T>(key, 0u) < (T)0.5) ? 1 : -1;  // direction of doubling 0 (:783-784)
+      v = (srec ? (dirb & 1u) != 0 : nuts_u<T>(key, 0u) < (T)0.5) ? 1 : -1;  // doubling 0's direction (:783-784)
       starting = false;
       continue;
     }
@@ -1199,7 +1221,9 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     const T joint = lp - kin;
     tn = (logu < joint) ? 1 : 0;
     ts = (logu - (T)1000) < joint;
-    ta = rust_min1(gexp(joint - joint0, ek));
+    // min(1, exp(joint - joint0)): f64 by the division-free table form
+    if constexpr (sizeof(T) == 8) ta = leaf_alpha_tab(joint - joint0, exp_lds, lek);
+    else ta = rust_min1(gexp(joint - joint0));
     tna = 1;
 #pragma unroll
     for (int e = 0; e < E; ++e) { fq[e] = qe[e]; fp[e] = pe[e]; pr[e] = qe[e]; }
@@ -1307,7 +1331,8 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       }
       ++j;
       if (s_ok && j < a.max_depth) {  // next doubling
-        const int v2 = (nuts_u<T>(key, 2u * (uint32_t)j) < (T)0.5) ? 1 : -1;
+        const bool up = srec ? ((dirb >> j) & 1u) != 0 : nuts_u<T>(key, 2u * (uint32_t)j) < (T)0.5;
+        const int v2 = up ? 1 : -1;
         const bool sw = v2 != v;  // integrate from the other end
 #pragma unroll
         for (int e = 0; e < E; ++e) {

@@ -187,6 +187,31 @@ __global__ void nuts_momenta_kernel(uint64_t seed, uint32_t chain_offset, uint64
   }
 }
 
+// Each transition's start record (nuts_device.h, transition start and
+// doubling ends): the TAG_NUTS_EXP block's stream key, ln of its Exp1
+// uniform and the direction bits of doublings 0..max_depth-1 -- a Philox
+// block, a log and max_depth hashes that a starting chain's wave otherwise
+// waits for in the tree kernel. The same functions, so the same bits.
+template <class T>
+__global__ void nuts_starts_kernel(uint64_t seed, uint32_t chain_offset, uint64_t step0, long long n, long long C,
+                                   int max_depth, uint64_t* __restrict__ key, T* __restrict__ lnu,
+                                   uint32_t* __restrict__ dir) {
+  const long long total = n * C;
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+       k += (long long)gridDim.x * blockDim.x) {
+    const long long c = k % C;
+    const uint64_t st = step0 + (uint64_t)(k / C);
+    const u32x4 kw = draw_block(seed, chain_offset + (uint32_t)c, st, TAG_NUTS_EXP, 0u);
+    const uint64_t K = nuts_key(kw);
+    uint32_t bits = 0;
+    for (int j = 0; j < max_depth && j < 32; ++j)
+      bits |= (nuts_u<T>(K, 2u * (uint32_t)j) < (T)0.5) ? (1u << j) : 0u;
+    key[k] = K;
+    lnu[k] = glog_pos(Unif<T>::oc(kw.z, kw.w));
+    dir[k] = bits;
+  }
+}
+
 template <class T>
 __global__ void nuts_fill_kernel(T* eps, T* eps_bar, T* h_bar, T* mu, long long C) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -534,7 +559,12 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     // (same values; skipped past GM_NUTS_ZBUF_MAX bytes, the kernel then draws
     // them itself), timed with the launch
     {
-      const size_t zb = (size_t)(nst > 0 ? nst : 0) * (size_t)C * (size_t)D * esz;
+      // [nst][C][D] momenta, then the start records' keys, logs and direction
+      // bits ([nst][C] each, 16-byte aligned)
+      const size_t nsc = (size_t)(nst > 0 ? nst : 0) * (size_t)C;
+      const size_t zmb = (nsc * (size_t)D * esz + 15) / 16 * 16;
+      const size_t zkb = (nsc * 8 + 15) / 16 * 16, zlb = (nsc * esz + 15) / 16 * 16;
+      const size_t zb = zmb + zkb + zlb + nsc * 4;
       if (ns.momentum_pass && zb > 0 && zb <= (size_t)GM_NUTS_ZBUF_MAX) {
         if (zb > ns.zbuf_bytes) {
           if (ns.zbuf) hipFree(ns.zbuf);
@@ -555,13 +585,26 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
           const long long nb = (long long)((a.step0 + (uint64_t)nst - 1) / S - a.step0 / S + 1);
           const long long work = nb * C * D;
           const unsigned zbk = (unsigned)((work + 255) / 256 < 65536 ? (work + 255) / 256 : 65536);
-          if (dt == GM_F32)
+          char* zp = (char*)ns.zbuf;
+          uint64_t* zk = (uint64_t*)(zp + zmb);
+          void* zl = zp + zmb + zkb;
+          uint32_t* zd = (uint32_t*)(zp + zmb + zkb + zlb);
+          const unsigned sbk = (unsigned)((nsc + 255) / 256 < 65536 ? (nsc + 255) / 256 : 65536);
+          if (dt == GM_F32) {
             hipLaunchKernelGGL(nuts_momenta_kernel<float>, dim3(zbk), dim3(256), 0, st, seed, chain_offset, a.step0,
                                nst, C, D, (float*)ns.zbuf);
-          else
+            hipLaunchKernelGGL(nuts_starts_kernel<float>, dim3(sbk), dim3(256), 0, st, seed, chain_offset, a.step0,
+                               nst, C, ns.max_depth, zk, (float*)zl, zd);
+          } else {
             hipLaunchKernelGGL(nuts_momenta_kernel<double>, dim3(zbk), dim3(256), 0, st, seed, chain_offset,
                                a.step0, nst, C, D, (double*)ns.zbuf);
+            hipLaunchKernelGGL(nuts_starts_kernel<double>, dim3(sbk), dim3(256), 0, st, seed, chain_offset,
+                               a.step0, nst, C, ns.max_depth, zk, (double*)zl, zd);
+          }
           a.zmom = ns.zbuf;
+          a.zkey = zk;
+          a.zlnu = zl;
+          a.zdir = zd;
         }
       }
     }

@@ -135,6 +135,28 @@ double or_exp_d(double x) {
   double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
   return scale2_d(y, k);
 }
+/* The NUTS leaf's acceptance statistic in f64, min(1, exp(x)) (generic_nuts.rs
+ * :1212; NaN gives 1), the kernels' division-free form (gm_rng.h
+ * leaf_alpha_tab): exp(max(min(x, 0), -746)) with k = rint(64 x / ln2),
+ * r = x - k ln2/64 by two fmas, exp(r) - 1 to degree 6, and 2^(j/64) from the
+ * table GM_EXP64_INIT (gm_bm_tables.h). fmin/fmax return the non-NaN
+ * operand, as the device's min/max do. */
+#include "gm_bm_tables.h"
+static const double exp64_tab[64] = {GM_EXP64_INIT};
+double or_leaf_alpha_d(double x) {
+  const double xs = fmax(fmin(x, 0.0), -746.0);
+  const double dk = rint(xs * 0x1.71547652b82fep+6);
+  const int k = (int)dk;
+  double r = fma(-dk, 0x1.62e42fee00000p-7, xs);
+  r = fma(-dk, 0x1.a39ef35793c76p-39, r);
+  double a = fma(r, 0x1.6c16c16c16c17p-10, 0x1.1111111111111p-7);
+  a = fma(r, a, 0x1.5555555555555p-5);
+  a = fma(r, a, 0x1.5555555555555p-3);
+  a = fma(r, a, 0.5);
+  const double p = fma(r * r, a, r);
+  const double tv = exp64_tab[k & 63];
+  return ldexp(fma(tv, p, tv), k >> 6);
+}
 static float scale2_f(float y, int k) {
   if (k > 127) return y * from_bits_f(0x7f000000u) * from_bits_f((uint32_t)(k) << 23);
   if (k < -125) return y * from_bits_f((uint32_t)(k + 100 + 127) << 23) * from_bits_f((uint32_t)(27) << 23);

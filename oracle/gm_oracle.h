@@ -47,6 +47,7 @@ void or_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 double or_log_d(double x);
 float or_log_f(float x);
 double or_exp_d(double x);
+double or_leaf_alpha_d(double x); /* the NUTS leaf's f64 min(1, exp(x)), the kernels' table form */
 float or_exp_f(float x);
 double or_cos2pi_d(double u);
 float or_cos2pi_f(float u);

@@ -51,6 +51,8 @@ def load():
         getattr(lib, f"or_mom_normal_{sfx}").restype = rt
         getattr(lib, f"or_mom_normal_{sfx}").argtypes = [_u64, _u32, _u64, _u32, _u32]
         if sfx == "d":
+            lib.or_leaf_alpha_d.restype = rt
+            lib.or_leaf_alpha_d.argtypes = [rt]
             lib.or_tab_normal_d.restype = rt
             lib.or_tab_normal_d.argtypes = [_u64, _u32, _u64, _u32, _u32]
             lib.or_tab_normal_pair.restype = None

@@ -41,6 +41,24 @@ def test_log_exp_within_one_ulp(oracle):
     assert oracle.lib.or_log_d(5e-324) == pytest.approx(math.log(5e-324), rel=1e-15)
 
 
+def test_leaf_alpha_table_exp(oracle):
+    """The NUTS leaf's f64 min(1, exp(x)) (gm_rng.h leaf_alpha_tab): within
+    1 ulp of exp over the normal range and 1 ulp of the smallest subnormal
+    below it; exactly 1 for x >= 0 and NaN (Rust's f64::min), +0 below -746."""
+    f = oracle.lib.or_leaf_alpha_d
+    rng = np.random.default_rng(1)
+    for x in (rng.uniform(-1, 0, 4000), rng.uniform(-708, 0, 4000), -rng.exponential(1e-3, 2000),
+              -np.arange(0, 64) * math.log(2) / 64, -np.arange(0, 1000) * math.log(2) / 128):
+        assert _ulps([f(v) for v in x], np.exp(x), np.float64) <= 1.0
+    sub = rng.uniform(-745.1, -708.5, 2000)
+    assert np.max(np.abs(np.array([f(v) for v in sub]) - np.exp(sub))) <= 5e-324
+    for v in (0.0, -0.0, 1e-300, 0.5, 3.0, 1e300, math.inf, math.nan):
+        assert f(v) == 1.0
+    for v in (-746.0, -746.5, -1e5, -math.inf):
+        assert f(v) == 0.0
+    assert f(-745.0) == np.exp(-745.0) and f(-1e-300) == 1.0
+
+
 def test_cos2pi_accuracy(oracle):
     u = np.linspace(0, 1, 5001, endpoint=False)
     assert np.max(np.abs(np.array([oracle.lib.or_cos2pi_d(v) for v in u]) - np.cos(2 * np.pi * u))) < 2e-15
