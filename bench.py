@@ -781,6 +781,12 @@ def main(argv=None, backend=None):
     offset, C_loc = shard(C_glob, world, rank)
     x0 = be.init_positions(C_glob, offset, C_loc)
     sampler = be.sampler(x0, offset)
+    # the measured sampler's runs are asynchronous: run_positions returns once
+    # the launch is enqueued, and the timed region's closing device
+    # synchronize is its one wait (0.7 us less host path than a stream wait
+    # followed by it, profiles/r06/host_path_probe.log V1 vs V2)
+    if hasattr(sampler, "set_async"):
+        sampler.set_async(True)
     lanes, elems = sampler.layout()
     comm = be.comm()
     if world > 1 and (comm is None or comm.info()["nranks"] != world):

@@ -55,57 +55,18 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
   T lp = tg.template eval<LPC, E, true>(x, gdummy, lane);
   long long acc = 0;
   NormalCache<T> ncache[E];  // f32: msun Box-Muller
-  // f64: the table-driven Box-Muller pair of each coordinate's current block
-  // (two steps), as plain per-coordinate values (selected, never indexed)
-  double tz0[E], tz1[E];
-  uint64_t tb = ~0ull;  // the block index (st / 2) the pairs belong to
-#pragma unroll
-  for (int e = 0; e < E; ++e) tz0[e] = tz1[e] = 0.0;
   UniformCache<T> ucache;
   uint64_t lblk = ~0ull;  // LPC == 64: the 64-step window whose accept logs lnl holds (lane k: step 64 lblk + k)
   T lnl = (T)0;
   const bool track = a.trk.mean != nullptr;  // run_progress (core.rs:146-163)
   ChainTrack<LPC, E> tr;
   if (track) tr.load(a.trk, c, lane, D);
-  for (int s = 0; s < a.n_steps; ++s) {
+  // one step from x given its proposal normals z (+0 in padded slots, whose
+  // y = +0 + +0 * sd then stays +0)
+  auto step = [&](int s, const T (&z)[E]) __attribute__((always_inline)) {
     const uint64_t st = a.step0 + (uint64_t)s;
-    T qpart = (T)0;
-    T ex[E];
-    bool qbad = false;
-    // f64: the coordinates' pairs are all fresh at the same steps (the block
-    // index is the lane-independent st / 2), one wave-uniform test
-    const bool fresh = TAB && (st / 2 != tb);
-    if constexpr (TAB) {
-      // the lane's E blocks and pairs issued side by side (draw_blocks_v,
-      // normals_tab_n): the E coordinates' Philox and Box-Muller chains are
-      // independent, so one chain's f64 latency is covered by the others'
-      // instructions (1.414e9 -> 1.432e9 chain-steps/s against drawing each
-      // coordinate's pair in its own branch, profiles/r06/ab_mh_draw_forms.log)
-      if (fresh) {
-        u32x4 w[E];
-        double z0[E], z1[E];
-        draw_blocks_v<E>(w, a.seed, cid, st / 2, TAG_MH_PROP, (uint32_t)(lane * E));
-        normals_tab_n<E>(w, z0, z1, bm_lds[0]);
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const bool in = lane * E + e < D;
-          tz0[e] = in ? z0[e] : 0.0;
-          tz1[e] = in ? z1[e] : 0.0;
-        }
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const int i = lane * E + e;
-      if constexpr (TAB) {
-        // (a padded slot keeps its pair at +0, so its y = +0 + +0 * sd = +0:
-        // no branch around the proposal, only around the draw)
-        y[e] = x[e] + ((st & 1u) ? tz1[e] : tz0[e]) * sd;
-      } else {
-        y[e] = (i < D) ? x[e] + ncache[e].get(a.seed, cid, st, TAG_MH_PROP, (uint32_t)i) * sd : (T)0;
-      }
-    }
-    if constexpr (TAB) tb = st / 2;
+    for (int e = 0; e < E; ++e) y[e] = x[e] + z[e] * sd;
     T lp1, log_alpha;
     if (cancel) {
       // the symmetric proposal's log q terms cancel (see above): the target's
@@ -113,6 +74,8 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
       lp1 = tg.finish(group_sum<LPC>(tg.template eval_part<LPC, E>(y, gdummy, lane)));
       log_alpha = lp1 - lp;
     } else {
+      T ex[E];
+      bool qbad = false;
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const int i = lane * E + e;
@@ -131,8 +94,9 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
           if (i < D) ex[e] = -(d * d) / two_var;
         }
       }
+      T qpart = ex[0];
 #pragma unroll
-      for (int e = 0; e < E; ++e) qpart = (e == 0) ? ex[e] : qpart + ex[e];
+      for (int e = 1; e < E; ++e) qpart = qpart + ex[e];
       // the proposal density's sum and the target's, reduced together: the
       // same stages (and bits) as two group_sums, each stage's DPP latency
       // covered by the other sum instead of wait states
@@ -182,6 +146,50 @@ __global__ __launch_bounds__(256) void mh_kernel(MhLaunch a, TG tg_) {
         const int i = lane * E + e;
         if (i < D) out[i] = x[e];
       }
+    }
+  };
+  if constexpr (TAB) {
+    // f64: one Philox block and Box-Muller pair per coordinate serve the steps
+    // st = 2b (z0) and 2b + 1 (z1); the loop takes the block's steps in turn,
+    // so each step reads its normals without a select. The lane's E blocks and
+    // pairs are issued side by side (draw_blocks_v, normals_tab_n): the E
+    // coordinates' Philox and Box-Muller chains are independent, so one
+    // chain's f64 latency is covered by the others' instructions (1.414e9 ->
+    // 1.432e9 chain-steps/s against each coordinate's pair in its own branch,
+    // profiles/r06/ab_mh_draw_forms.log).
+    for (int s = 0; s < a.n_steps;) {
+      const uint64_t st = a.step0 + (uint64_t)s;
+      u32x4 w[E];
+      double z0[E], z1[E];
+      draw_blocks_v<E>(w, a.seed, cid, st / 2, TAG_MH_PROP, (uint32_t)(lane * E));
+      normals_tab_n<E>(w, z0, z1, bm_lds[0]);
+      if (D < LPC * E) {  // padded slots (wave-uniform): their normals +0
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const bool in = lane * E + e < D;
+          z0[e] = in ? z0[e] : 0.0;
+          z1[e] = in ? z1[e] : 0.0;
+        }
+      }
+      if ((st & 1u) == 0) {
+        step(s, z0);
+        ++s;
+      }
+      if (s < a.n_steps) {
+        step(s, z1);
+        ++s;
+      }
+    }
+  } else {
+    for (int s = 0; s < a.n_steps; ++s) {
+      const uint64_t st = a.step0 + (uint64_t)s;
+      T z[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const int i = lane * E + e;
+        z[e] = (i < D) ? ncache[e].get(a.seed, cid, st, TAG_MH_PROP, (uint32_t)i) : (T)0;
+      }
+      step(s, z);
     }
   }
 #pragma unroll

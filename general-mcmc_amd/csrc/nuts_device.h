@@ -972,8 +972,11 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   T joint0 = (T)0, logu = (T)0;
   uint64_t key = 0;
   uint32_t dirb = 0;  // the transition's direction bits (pre-pass record)
+// The frozen-dense kernel keeps its in-kernel start draws: with the records
+// its spills grew (61 -> 73 VGPRs) and cfg3_dense ran 1.7 % slower, against
+// +2.6 % for cfg3 (profiles/r06/ab_nuts_start_records.log).
 #ifndef GM_SREC_DENSE
-#define GM_SREC_DENSE 1  // the frozen-dense kernel reads the start records too
+#define GM_SREC_DENSE 0
 #endif
   uint32_t merge_ctr = 0;
   T fq[E], fp[E], pr[E];  // current subtree: first q, first p, proposal
