@@ -36,8 +36,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, spec)
 VALU_F32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md, spec)
 VALU_F64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (MI355X_MICROARCH.md, spec)
 METRIC = "leapfrog steps/sec (whole node) + ESS/sec, 64-dim Rosenbrock HMC at 1/2/4/8 GPUs"
-PMC_FILE = os.path.join(ROOT, "profiles", "r05", "pmc_hmc.json")
-PMC_CONFIGS_FILE = os.path.join(ROOT, "profiles", "r05", "pmc_configs.json")  # tools/profile_r05.sh
+PMC_FILE = os.path.join(ROOT, "profiles", "r06", "pmc_hmc.json")
+PMC_CONFIGS_FILE = os.path.join(ROOT, "profiles", "r06", "pmc_configs.json")  # tools/profile_r06.sh
 
 
 def parse(argv=None):

@@ -129,12 +129,18 @@ struct NutsLaunch {
   // draw), or null: drawn in the kernel
   const void* zmom = nullptr;
   // with zmom, each transition's start record from the same pass
-  // (nuts_starts_kernel, [n_steps][C] each): the stream key K of the
-  // TAG_NUTS_EXP block, ln of its Exp1 uniform, and the doublings' direction
-  // bits (bit j: u(K, 2j) < 1/2) -- the values the kernel would compute
-  const uint64_t* zkey = nullptr;
-  const void* zlnu = nullptr;
-  const uint32_t* zdir = nullptr;
+  // (nuts_starts_kernel, [n_steps][C] of NutsStartRec<T>): the stream key K
+  // of the TAG_NUTS_EXP block, ln of its Exp1 uniform, and the doublings'
+  // direction bits (bit j: u(K, 2j) < 1/2) -- the values the kernel would
+  // compute
+  const void* zrec = nullptr;
+};
+// one start record: 16 bytes (f32) or 32 (f64), read as one 16-byte load
+// (key, ln u) and, in f64, one 4-byte load (the direction bits)
+template <class T> struct alignas(16) NutsStartRec {
+  uint64_t key;
+  T lnu;
+  uint32_t dir;
 };
 
 // waves per SIMD of the NUTS dense-metric instantiations (their launch

@@ -1012,7 +1012,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   // would also wait out the previous transition's sample stores.
   __builtin_amdgcn_s_waitcnt(0);
   const LeafExpK lek = LeafExpK::make();  // the leaf exp's constants (f64)
-  // the launch's start records from the momentum pre-pass (a.zkey ...)
+  // the launch's start records from the momentum pre-pass (a.zrec)
   const bool srec = (GM_SREC_DENSE || MASS != 3) && a.zmom != nullptr;
   while (true) {
     const bool live = s < a.n_steps;
@@ -1061,10 +1061,13 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     // below), else drawn here; the metric's product after the evaluation
     T zs[E];
     // with the pre-pass: the transition's start record as well (its key, the
-    // slice variable's log and the direction bits), loaded with the momenta
-    uint64_t skey = 0;
-    T slnu = (T)0;
-    uint32_t sdir = 0;
+    // slice variable's log and the direction bits), loaded with the momenta.
+    // (Left unset otherwise, like zs: zeroing them would make the loop head
+    // wait for the previous iteration's loads into the same registers, and on
+    // gfx9 that vmcnt wait includes every outstanding store.)
+    uint64_t skey;
+    T slnu;
+    uint32_t sdir;
     if (live && starting) {
       if (a.zmom != nullptr) {
         const T* __restrict__ zm = (const T*)a.zmom + ((long long)s * C + c) * D;
@@ -1074,9 +1077,10 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
           zs[e] = (i < D) ? zm[i] : (T)0;
         }
         if (srec) {
-          skey = a.zkey[(long long)s * C + c];
-          slnu = ((const T*)a.zlnu)[(long long)s * C + c];
-          sdir = a.zdir[(long long)s * C + c];
+          const NutsStartRec<T>* __restrict__ r = (const NutsStartRec<T>*)a.zrec + ((long long)s * C + c);
+          skey = r->key;
+          slnu = r->lnu;
+          sdir = r->dir;
         }
       } else {
 #pragma unroll

@@ -194,8 +194,7 @@ __global__ void nuts_momenta_kernel(uint64_t seed, uint32_t chain_offset, uint64
 // waits for in the tree kernel. The same functions, so the same bits.
 template <class T>
 __global__ void nuts_starts_kernel(uint64_t seed, uint32_t chain_offset, uint64_t step0, long long n, long long C,
-                                   int max_depth, uint64_t* __restrict__ key, T* __restrict__ lnu,
-                                   uint32_t* __restrict__ dir) {
+                                   int max_depth, NutsStartRec<T>* __restrict__ rec) {
   const long long total = n * C;
   for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < total;
        k += (long long)gridDim.x * blockDim.x) {
@@ -206,9 +205,11 @@ __global__ void nuts_starts_kernel(uint64_t seed, uint32_t chain_offset, uint64_
     uint32_t bits = 0;
     for (int j = 0; j < max_depth && j < 32; ++j)
       bits |= (nuts_u<T>(K, 2u * (uint32_t)j) < (T)0.5) ? (1u << j) : 0u;
-    key[k] = K;
-    lnu[k] = glog_pos(Unif<T>::oc(kw.z, kw.w));
-    dir[k] = bits;
+    NutsStartRec<T> r;
+    r.key = K;
+    r.lnu = glog_pos(Unif<T>::oc(kw.z, kw.w));
+    r.dir = bits;
+    rec[k] = r;
   }
 }
 
@@ -559,12 +560,10 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
     // (same values; skipped past GM_NUTS_ZBUF_MAX bytes, the kernel then draws
     // them itself), timed with the launch
     {
-      // [nst][C][D] momenta, then the start records' keys, logs and direction
-      // bits ([nst][C] each, 16-byte aligned)
+      // [nst][C][D] momenta, then the start records [nst][C] (16-byte aligned)
       const size_t nsc = (size_t)(nst > 0 ? nst : 0) * (size_t)C;
       const size_t zmb = (nsc * (size_t)D * esz + 15) / 16 * 16;
-      const size_t zkb = (nsc * 8 + 15) / 16 * 16, zlb = (nsc * esz + 15) / 16 * 16;
-      const size_t zb = zmb + zkb + zlb + nsc * 4;
+      const size_t zb = zmb + nsc * (dt == GM_F32 ? sizeof(NutsStartRec<float>) : sizeof(NutsStartRec<double>));
       if (ns.momentum_pass && zb > 0 && zb <= (size_t)GM_NUTS_ZBUF_MAX) {
         if (zb > ns.zbuf_bytes) {
           if (ns.zbuf) hipFree(ns.zbuf);
@@ -585,26 +584,21 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
           const long long nb = (long long)((a.step0 + (uint64_t)nst - 1) / S - a.step0 / S + 1);
           const long long work = nb * C * D;
           const unsigned zbk = (unsigned)((work + 255) / 256 < 65536 ? (work + 255) / 256 : 65536);
-          char* zp = (char*)ns.zbuf;
-          uint64_t* zk = (uint64_t*)(zp + zmb);
-          void* zl = zp + zmb + zkb;
-          uint32_t* zd = (uint32_t*)(zp + zmb + zkb + zlb);
+          void* zr = (char*)ns.zbuf + zmb;
           const unsigned sbk = (unsigned)((nsc + 255) / 256 < 65536 ? (nsc + 255) / 256 : 65536);
           if (dt == GM_F32) {
             hipLaunchKernelGGL(nuts_momenta_kernel<float>, dim3(zbk), dim3(256), 0, st, seed, chain_offset, a.step0,
                                nst, C, D, (float*)ns.zbuf);
             hipLaunchKernelGGL(nuts_starts_kernel<float>, dim3(sbk), dim3(256), 0, st, seed, chain_offset, a.step0,
-                               nst, C, ns.max_depth, zk, (float*)zl, zd);
+                               nst, C, ns.max_depth, (NutsStartRec<float>*)zr);
           } else {
             hipLaunchKernelGGL(nuts_momenta_kernel<double>, dim3(zbk), dim3(256), 0, st, seed, chain_offset,
                                a.step0, nst, C, D, (double*)ns.zbuf);
             hipLaunchKernelGGL(nuts_starts_kernel<double>, dim3(sbk), dim3(256), 0, st, seed, chain_offset,
-                               a.step0, nst, C, ns.max_depth, zk, (double*)zl, zd);
+                               a.step0, nst, C, ns.max_depth, (NutsStartRec<double>*)zr);
           }
           a.zmom = ns.zbuf;
-          a.zkey = zk;
-          a.zlnu = zl;
-          a.zdir = zd;
+          a.zrec = zr;
         }
       }
     }

@@ -6,4 +6,4 @@ run forms_tests 400 python -u -m pytest tests/test_gpu_forms.py -x -v -s --timeo
 AB_ROUNDS=3 run ab_mh 400 python tools/ab_mh.py abtest/mh_f0/libgmcmc.so abtest/mh_f1/libgmcmc.so general-mcmc_amd/lib/libgmcmc.so || exit $?
 AB_ROUNDS=3 run ab_nuts 300 python tools/ab_nuts.py abtest/nuts_u0/libgmcmc.so general-mcmc_amd/lib/libgmcmc.so || exit $?
 AB_ARGS="--nuts-mass dense" AB_ROUNDS=2 run ab_dense 300 python tools/ab_nuts.py abtest/nuts_u0/libgmcmc.so general-mcmc_amd/lib/libgmcmc.so || exit $?
-tail -8 gpurun_out/ab_mh.log gpurun_out/ab_nuts.log gpurun_out/ab_dense.log
+tail -n 8 gpurun_out/ab_mh.log gpurun_out/ab_nuts.log gpurun_out/ab_dense.log

@@ -13,4 +13,4 @@ AB_ROUNDS=3 run ab_nuts 400 python tools/ab_nuts.py abrun/nuts_u0/libgmcmc.so $L
 AB_ARGS="--nuts-mass dense" AB_ROUNDS=2 run ab_dense 450 python tools/ab_nuts.py $L abrun/pf0/libgmcmc.so \
   abrun/pf1/libgmcmc.so abrun/pf2/libgmcmc.so || exit $?
 run forms_tests 300 python -u -m pytest tests/test_gpu_forms.py -x -v -s --timeout 200 --timeout-method thread || exit $?
-tail -6 gpurun_out/ab_mh.log gpurun_out/ab_nuts.log gpurun_out/ab_dense.log
+tail -n 6 gpurun_out/ab_mh.log gpurun_out/ab_nuts.log gpurun_out/ab_dense.log

@@ -8,4 +8,4 @@ run gpu_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 AB_ROUNDS=3 run ab_nuts 400 python tools/ab_nuts.py abrun/base/libgmcmc.so $L abrun/lexp_pin1/libgmcmc.so || exit $?
 AB_ARGS="--nuts-mass dense" AB_ROUNDS=2 run ab_dense 450 python tools/ab_nuts.py abrun/base/libgmcmc.so $L \
   abrun/lexp_pin1/libgmcmc.so || exit $?
-tail -12 gpurun_out/ab_nuts.log gpurun_out/ab_dense.log
+tail -n 12 gpurun_out/ab_nuts.log gpurun_out/ab_dense.log

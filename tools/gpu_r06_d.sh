@@ -12,6 +12,6 @@ AB_ROUNDS=3 run ab_nuts 400 python tools/ab_nuts.py abrun/prev/libgmcmc.so $L ||
 AB_ARGS="--nuts-mass dense" AB_ROUNDS=2 run ab_dense 450 python tools/ab_nuts.py abrun/prev/libgmcmc.so $L \
   abrun/srec_d0/libgmcmc.so || exit $?
 run host_path 120 python tools/probe_host_path.py || exit $?
-tail -12 gpurun_out/ab_nuts.log gpurun_out/ab_dense.log
+tail -n 12 gpurun_out/ab_nuts.log gpurun_out/ab_dense.log
 AB_ROUNDS=3 run ab_mh 400 python tools/ab_mh.py abrun/prev/libgmcmc.so $L || exit $?
-tail -12 gpurun_out/ab_mh.log
+tail -n 12 gpurun_out/ab_mh.log
