@@ -68,6 +68,10 @@ def cfg3(a):
 def cfg4(a):
     C, D, L = a.hmc128_chains, 128, 50
     s = gm.HMC(gm.RosenbrockND(), gm.init_det(C, D, np.float32), 0.01, L).set_seed(42)
+    if a.hmc128_layout:
+        s.set_layout(*[int(v) for v in a.hmc128_layout.split("x")])
+    if a.hmc128_unroll:
+        s.set_unroll(a.hmc128_unroll)
     s.run_positions(0, 100)
     ds, t = timed(lambda: s.run_positions(100, 0))
     rhat, ess = ds.split_rhat_ess()
@@ -119,6 +123,8 @@ def main():
     p.add_argument("--nuts-collect", type=int, default=500)
     p.add_argument("--nuts-layout", default="")
     p.add_argument("--hmc128-chains", type=int, default=8192)
+    p.add_argument("--hmc128-layout", default="")
+    p.add_argument("--hmc128-unroll", type=int, default=0)
     p.add_argument("--mh-chains", type=int, default=16384)
     p.add_argument("--mh-layout", default="")
     a = p.parse_args()
