@@ -765,6 +765,22 @@ LEG_NOTES = {
 }
 
 
+def pin_host_thread(rank: int):
+    """The rank's host thread on one of the CPUs the process may use (the
+    rank-th) from the device warm-up to the end of the timed region, so that
+    the timed call's launch and spin-wait do not migrate between cores:
+    median host path 12.2 -> 10.8 us, headline +1.8 % over 5 alternating
+    rounds (profiles/r06/ab_bench_pin.jsonl). Returns the previous affinity
+    (restored before the CPU-baseline legs, whose threads need every core);
+    BENCH_PIN_CPU=0 turns it off."""
+    if os.environ.get("BENCH_PIN_CPU", "1") != "1" or not hasattr(os, "sched_setaffinity"):
+        return None
+    prev = os.sched_getaffinity(0)
+    cpus = sorted(prev)
+    os.sched_setaffinity(0, {cpus[rank % len(cpus)]})
+    return prev
+
+
 def main(argv=None, backend=None):
     a = parse(argv)
     from general_mcmc_amd.distributed import ControlPlane, shard
@@ -809,6 +825,7 @@ def main(argv=None, backend=None):
     # scratch launches the first call of a process is slower still
     # (profiles/r02/first_call/). The measured chains are exactly W
     # transitions from the start.
+    affinity = pin_host_thread(rank)
     scratch = be.sampler(x0, offset)
     scratch.reserve(a.steps)
     t_warm_end = time.perf_counter() + a.device_warmup_ms * 1e-3
@@ -826,6 +843,8 @@ def main(argv=None, backend=None):
     # and the max over ranks below is the slowest rank's time
     be.sync()
     t_local = time.perf_counter() - t0
+    if affinity is not None:
+        os.sched_setaffinity(0, affinity)
     cp.barrier()
     scratch.close()
     kernel_ms, launches = sampler.last_run_stats()
