@@ -766,27 +766,27 @@ LEG_NOTES = {
 
 
 def pin_host_thread(rank: int, world: int):
-    """The rank's host thread on one of the CPUs the process may use (the
-    rank-th) from the device warm-up to the end of the timed region, so that
-    the timed call's launch and spin-wait do not migrate between cores:
-    median host path 12.2 -> 10.8 us, headline +1.8 % over 5 alternating
-    rounds (profiles/r06/ab_bench_pin.jsonl); pinned to the current CPU,
-    13.7 -> 11.1 us, +3 % (ab_bench_pin_current_cpu.jsonl). Returns the previous affinity
-    (restored before the CPU-baseline legs, whose threads need every core);
-    BENCH_PIN_CPU=0 turns it off."""
-    if os.environ.get("BENCH_PIN_CPU", "1") != "1" or not hasattr(os, "sched_setaffinity"):
+    """A single rank's host thread on the CPU it runs on, from the device
+    warm-up to the end of the timed region, so that the timed call's launch
+    and spin-wait do not migrate between cores: median host path 12.2 ->
+    10.8 us, headline +1.8 % over 5 alternating rounds
+    (profiles/r06/ab_bench_pin.jsonl, the first allowed CPU); the current
+    CPU, 13.7 -> 11.1 us, +3 % (ab_bench_pin_current_cpu.jsonl). Returns the
+    previous affinity (restored before the CPU-baseline legs, whose threads
+    need every core); BENCH_PIN_CPU=0 turns it off."""
+    # (one rank only: several ranks would need their GPUs' NUMA-near cores,
+    # which the first allowed CPUs need not be)
+    if os.environ.get("BENCH_PIN_CPU", "1") != "1" or world != 1 or not hasattr(os, "sched_setaffinity"):
         return None
     prev = os.sched_getaffinity(0)
-    cpus = sorted(prev)
-    cpu = cpus[rank % len(cpus)]
-    if world == 1:  # one rank: the CPU it runs on now (no migration, warm caches)
-        try:
-            import ctypes
-            now = ctypes.CDLL(None).sched_getcpu()
-            if now in prev:
-                cpu = now
-        except (OSError, AttributeError):
-            pass
+    cpu = sorted(prev)[0]
+    try:  # the CPU it runs on now (no migration, warm caches)
+        import ctypes
+        now = ctypes.CDLL(None).sched_getcpu()
+        if now in prev:
+            cpu = now
+    except (OSError, AttributeError):
+        pass
     os.sched_setaffinity(0, {cpu})
     return prev
 
