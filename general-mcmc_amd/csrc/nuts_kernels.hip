@@ -586,19 +586,23 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
           const unsigned zbk = (unsigned)((work + 255) / 256 < 65536 ? (work + 255) / 256 : 65536);
           void* zr = (char*)ns.zbuf + zmb;
           const unsigned sbk = (unsigned)((nsc + 255) / 256 < 65536 ? (nsc + 255) / 256 : 65536);
+          // (the frozen-dense kernel draws its starts itself: GM_SREC_DENSE)
+          const bool recs = !(a.mass_mode == 2 && a.dense_frozen && !GM_SREC_DENSE);
           if (dt == GM_F32) {
             hipLaunchKernelGGL(nuts_momenta_kernel<float>, dim3(zbk), dim3(256), 0, st, seed, chain_offset, a.step0,
                                nst, C, D, (float*)ns.zbuf);
-            hipLaunchKernelGGL(nuts_starts_kernel<float>, dim3(sbk), dim3(256), 0, st, seed, chain_offset, a.step0,
-                               nst, C, ns.max_depth, (NutsStartRec<float>*)zr);
+            if (recs)
+              hipLaunchKernelGGL(nuts_starts_kernel<float>, dim3(sbk), dim3(256), 0, st, seed, chain_offset, a.step0,
+                                 nst, C, ns.max_depth, (NutsStartRec<float>*)zr);
           } else {
             hipLaunchKernelGGL(nuts_momenta_kernel<double>, dim3(zbk), dim3(256), 0, st, seed, chain_offset,
                                a.step0, nst, C, D, (double*)ns.zbuf);
-            hipLaunchKernelGGL(nuts_starts_kernel<double>, dim3(sbk), dim3(256), 0, st, seed, chain_offset,
-                               a.step0, nst, C, ns.max_depth, (NutsStartRec<double>*)zr);
+            if (recs)
+              hipLaunchKernelGGL(nuts_starts_kernel<double>, dim3(sbk), dim3(256), 0, st, seed, chain_offset,
+                                 a.step0, nst, C, ns.max_depth, (NutsStartRec<double>*)zr);
           }
           a.zmom = ns.zbuf;
-          a.zrec = zr;
+          a.zrec = recs ? zr : nullptr;
         }
       }
     }
