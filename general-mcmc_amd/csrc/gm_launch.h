@@ -134,7 +134,20 @@ struct NutsLaunch {
   // direction bits (bit j: u(K, 2j) < 1/2) -- the values the kernel would
   // compute
   const void* zrec = nullptr;
+  // frozen-dense launches (MASS 3) with zmom: the pass has also applied the
+  // metric (nuts_dense_momenta_kernel), so zmom holds the momenta p0 = L z
+  // themselves and pv0 their M^-1 p0, [n_steps][C][D] each -- the products
+  // sample_momentum and the start's kinetic energy would otherwise take in
+  // the tree kernel, with the same sums in the same order. Null: the kernel
+  // applies L and M^-1 to zmom's normals itself.
+  const void* pv0 = nullptr;
 };
+// the frozen-dense kernel takes its momenta from the pass (pv0 always set;
+// nuts_run launches it for no other launch). 0: A/B builds only, the kernel
+// applies the metric itself when pv0 is null
+#ifndef GM_DENSE_PREP
+#define GM_DENSE_PREP 1
+#endif
 // one start record: 16 bytes (f32) or 32 (f64), read as one 16-byte load
 // (key, ln u) and, in f64, one 4-byte load (the direction bits)
 template <class T> struct alignas(16) NutsStartRec {

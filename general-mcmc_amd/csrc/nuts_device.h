@@ -1014,6 +1014,10 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   const LeafExpK lek = LeafExpK::make();  // the leaf exp's constants (f64)
   // the launch's start records from the momentum pre-pass (a.zrec)
   const bool srec = (GM_SREC_DENSE || MASS != 3) && a.zmom != nullptr;
+  // the frozen-dense kernel's momenta with the metric applied (a.pv0)
+  // (known at compile time in the default build: no in-kernel draw, L
+  // product or start-time M^-1 product is emitted there)
+  const bool prepd = MASS == 3 && (GM_DENSE_PREP || a.pv0 != nullptr);
   while (true) {
     const bool live = s < a.n_steps;
 #ifdef GM_NUTS_PROF
@@ -1069,18 +1073,28 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     T slnu;
     uint32_t sdir;
     if (live && starting) {
-      if (a.zmom != nullptr) {
+      if (srec) {
+        const NutsStartRec<T>* __restrict__ r = (const NutsStartRec<T>*)a.zrec + ((long long)s * C + c);
+        skey = r->key;
+        slnu = r->lnu;
+        sdir = r->dir;
+      }
+      if (prepd) {  // p0 and M^-1 p0 from the pre-pass (a.pv0)
+        const long long o = ((long long)s * C + c) * D;
+        const T* __restrict__ pm = (const T*)a.zmom + o;
+        const T* __restrict__ vm = (const T*)a.pv0 + o;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = lane * E + e;
+          p0l[e] = (i < D) ? pm[i] : (T)0;
+          v0l[e] = (i < D) ? vm[i] : (T)0;
+        }
+      } else if (a.zmom != nullptr) {
         const T* __restrict__ zm = (const T*)a.zmom + ((long long)s * C + c) * D;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           const int i = lane * E + e;
           zs[e] = (i < D) ? zm[i] : (T)0;
-        }
-        if (srec) {
-          const NutsStartRec<T>* __restrict__ r = (const NutsStartRec<T>*)a.zrec + ((long long)s * C + c);
-          skey = r->key;
-          slnu = r->lnu;
-          sdir = r->dir;
         }
       } else {
 #pragma unroll
@@ -1132,7 +1146,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
 #endif
 #pragma unroll
     for (int e = 0; e < E; ++e) pe[e] = pe[e] + gx[e] * h;  // (unconditionally, as above)
-    if (live && starting) momentum_from<LPC, E>(M, zs, p0, lane);  // sample_momentum (:275-303)
+    if (live && starting && !prepd) momentum_from<LPC, E>(M, zs, p0, lane);  // sample_momentum (:275-303)
     T wx[E];  // dense metric: M^-1 g at the evaluation point
     {
       T pk[E];
@@ -1144,7 +1158,8 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
         // chain's M^-1 p0 only in iterations where some chain of the wave
         // starts a transition
         inv_mul<LPC, E>(M, gx, wx, lane);
-        if (__builtin_amdgcn_ballot_w64(live && starting && M.kind() == 2) != 0) inv_mul<LPC, E>(M, p0, v0, lane);
+        if (!prepd && __builtin_amdgcn_ballot_w64(live && starting && M.kind() == 2) != 0)
+          inv_mul<LPC, E>(M, p0, v0, lane);
         if (M.kind() == 2) {
           T t[E];
 #pragma unroll

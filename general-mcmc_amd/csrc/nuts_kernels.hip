@@ -187,6 +187,73 @@ __global__ void nuts_momenta_kernel(uint64_t seed, uint32_t chain_offset, uint64
   }
 }
 
+// Frozen-dense launches: the metric applied to the pass's normals, for every
+// transition of the launch at once -- p0 = L z (sample_momentum,
+// generic_nuts.rs:275-303) in place of z, and M^-1 p0 (the start's kinetic
+// energy and carried velocity, :244-273) into v0 -- instead of at each
+// transition start inside the tree kernel, where L came from HBM on the
+// start's critical path and streamed 8 KiB per transition through the L2 the
+// subtree stack lives in. The sums are the tree kernel's (nuts_device.h
+// momentum_from / chol_global_cols and inv_mul / packed_cols): p_i from +0,
+// j ascending, a separate multiply and add (the build does not contract);
+// (M^-1 p)_i from +0 by fma, j ascending. The kernel's padded terms (j > i in
+// L, columns past D) add +-0 to a +0-started sum and change no bit, so they
+// are left out here. One block per chain: its L (transposed) and M^-1
+// (transposed, as the tree kernel's copy) staged in LDS once, then R = 256/D
+// transitions per round, thread (r, i) computing coordinate i of
+// transition s0 + r. Its LDS: nuts_dense_prep_lds (<= 64 KiB, else the tree
+// kernel applies the metric itself).
+static size_t nuts_dense_prep_lds(int D, size_t esz) {
+  if (D < 1 || D > 256) return 0;
+  const size_t b = (2 * (size_t)D * D + (size_t)(256 / D) * D) * esz;
+  return b <= 64 * 1024 ? b : 0;
+}
+template <class T>
+__global__ __launch_bounds__(256) void nuts_dense_momenta_kernel(long long n, long long C, int D,
+                                                                 const T* __restrict__ chol_rm,
+                                                                 const T* __restrict__ minvT, T* __restrict__ pz,
+                                                                 T* __restrict__ v0) {
+  extern __shared__ __align__(16) unsigned char dm_lds[];
+  T* lt = (T*)dm_lds;       // [j][i] = L_ij
+  T* mt = lt + D * D;       // [j][i] = M^-1_ij
+  T* zl = mt + D * D;       // [r][j] this round's normals, then momenta
+  const long long c = blockIdx.x;
+  const T* L = chol_rm + c * (long long)D * D;
+  const T* Mi = minvT + c * (long long)D * D;
+  for (int k = threadIdx.x; k < D * D; k += blockDim.x) {
+    const int i = k / D, j = k - i * D;
+    lt[j * D + i] = L[k];  // L row-major: k = i*D + j
+    mt[k] = Mi[k];
+  }
+  const int R = 256 / D;
+  const int r = threadIdx.x / D, i = threadIdx.x - r * D;
+  const bool act = r < R;
+  for (long long s0 = 0; s0 < n; s0 += R) {
+    const long long s = s0 + r;
+    const bool on = act && s < n;
+    const long long o = (s * C + c) * D + i;
+    __syncthreads();  // (the previous round's reads of zl are done)
+    if (on) zl[r * D + i] = pz[o];
+    __syncthreads();
+    T p = (T)0;
+    if (on) {
+      for (int j = 0; j <= i; ++j) p = p + lt[j * D + i] * zl[r * D + j];
+    }
+    __syncthreads();
+    if (on) zl[r * D + i] = p;
+    __syncthreads();
+    if (on) {
+      // the tree kernel's packed triangle: row i's entry j from M^-1_ij while
+      // j <= i, from M^-1_ji after (the same values: M^-1 is exactly
+      // symmetric, and this keeps the very same reads)
+      T w = (T)0;
+      for (int j = 0; j < D; ++j) w = gfma(j <= i ? mt[j * D + i] : mt[i * D + j], zl[r * D + j], w);
+      pz[o] = p;
+      v0[o] = w;
+    }
+  }
+}
+
 // Each transition's start record (nuts_device.h, transition start and
 // doubling ends): the TAG_NUTS_EXP block's stream key, ln of its Exp1
 // uniform and the direction bits of doublings 0..max_depth-1 -- a Philox
@@ -563,7 +630,19 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
       // [nst][C][D] momenta, then the start records [nst][C] (16-byte aligned)
       const size_t nsc = (size_t)(nst > 0 ? nst : 0) * (size_t)C;
       const size_t zmb = (nsc * (size_t)D * esz + 15) / 16 * 16;
-      const size_t zb = zmb + nsc * (dt == GM_F32 ? sizeof(NutsStartRec<float>) : sizeof(NutsStartRec<double>));
+      const size_t zrb = nsc * (dt == GM_F32 ? sizeof(NutsStartRec<float>) : sizeof(NutsStartRec<double>));
+      // a frozen-dense launch (the MASS 3 kernel, 16 x 2): the metric applied
+      // in the pass as well, M^-1 p0 [nst][C][D] after the records
+      // (the frozen kernel is built for this pass, GM_DENSE_PREP: a launch the
+      // pass cannot serve -- pass off, buffer past its cap or not allocated --
+      // takes the adaptive dense kernel instead, the same bits)
+      const size_t dpl = (a.mass_mode == 2 && a.dense_frozen) ? nuts_dense_prep_lds(D, esz) : 0;
+      const size_t zvo = (zmb + zrb + 15) / 16 * 16;
+      if (GM_DENSE_PREP && a.dense_frozen &&
+          !(dpl > 0 && C <= 0x7fffffff && ns.momentum_pass && zvo + zmb <= (size_t)GM_NUTS_ZBUF_MAX))
+        a.dense_frozen = 0;
+      const bool dprep = GM_DENSE_PREP && a.dense_frozen;
+      const size_t zb = dprep ? zvo + zmb : zmb + zrb;
       if (ns.momentum_pass && zb > 0 && zb <= (size_t)GM_NUTS_ZBUF_MAX) {
         if (zb > ns.zbuf_bytes) {
           if (ns.zbuf) hipFree(ns.zbuf);
@@ -601,10 +680,22 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
               hipLaunchKernelGGL(nuts_starts_kernel<double>, dim3(sbk), dim3(256), 0, st, seed, chain_offset,
                                  a.step0, nst, C, ns.max_depth, (NutsStartRec<double>*)zr);
           }
+          if (dprep) {  // p0 = L z in place of z, M^-1 p0 at zvo
+            void* pv = (char*)ns.zbuf + zvo;
+            if (dt == GM_F32)
+              hipLaunchKernelGGL(nuts_dense_momenta_kernel<float>, dim3((unsigned)C), dim3(256), dpl, st, nst, C, D,
+                                 (const float*)a.mchol_rm, (const float*)a.minv, (float*)ns.zbuf, (float*)pv);
+            else
+              hipLaunchKernelGGL(nuts_dense_momenta_kernel<double>, dim3((unsigned)C), dim3(256), dpl, st, nst, C,
+                                 D, (const double*)a.mchol_rm, (const double*)a.minv, (double*)ns.zbuf,
+                                 (double*)pv);
+            a.pv0 = pv;
+          }
           a.zmom = ns.zbuf;
           a.zrec = recs ? zr : nullptr;
         }
       }
+      if (GM_DENSE_PREP && a.dense_frozen && a.pv0 == nullptr) a.dense_frozen = 0;  // (no buffer)
     }
     hipError_t e;
     if (tg.kind == GM_TARGET_CUSTOM) {  // user target, runtime-compiled (gm_jit.cpp)

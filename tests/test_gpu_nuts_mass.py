@@ -19,7 +19,7 @@ def _gauss(gm, cov, mean=None):
     return gm.DenseGaussian(mean, cov)
 
 
-def _check_run(gm, oracle, t, x0, dtype, mode, runs, progress=False, layout=None, forms=None, **cfg):
+def _check_run(gm, oracle, t, x0, dtype, mode, runs, progress=False, layout=None, forms=None, mpass=True, **cfg):
     C_, D = x0.shape
     adapt = {1: "diagonal", 2: "dense"}[mode]
     mc = gm.NUTSMassMatrixConfig(adapt, **{**dict(regularize=0.05, jitter=1e-6, dense_max_dim=75), **cfg})
@@ -28,6 +28,8 @@ def _check_run(gm, oracle, t, x0, dtype, mode, runs, progress=False, layout=None
         s.set_layout(*layout)
     if forms:
         s.set_dense_forms(**forms)
+    if not mpass:
+        s.set_momentum_pass(False)
     lanes, elems = s.layout()
     ot = Target.from_product(t, D)
     st = oracle.nuts_state(C_, dtype)
@@ -119,22 +121,26 @@ def test_dense_warmup_matrix_core_layout(gm, oracle, minv_lds, chol_lds, D, chai
     assert plan["chol_lds"] <= int(chol_lds) and (plan["chol_lds"] == 0 or plan["minv_lds"] == 1)
 
 
-@pytest.mark.parametrize("D,chains,dtype", [(32, 36, np.float64), (20, 10, np.float64), (32, 36, np.float32)])
-def test_dense_frozen_sampling_bitexact(gm, oracle, D, chains, dtype):
+@pytest.mark.parametrize("D,chains,dtype,mpass", [(32, 36, np.float64, True), (20, 10, np.float64, True),
+                                                  (32, 36, np.float32, True), (32, 36, np.float64, False)])
+def test_dense_frozen_sampling_bitexact(gm, oracle, D, chains, dtype, mpass):
     """After the warm-up, a run without windows (run(n, 0), the bench's
     sampling phase) with every chain's metric dense takes the frozen-dense
     kernel (MASS 3: no identity/diagonal branches, no Welford state, two
-    waves per SIMD at 16 x 2) -- the same bits as the oracle, partial wave
-    included; a later warm-up run goes back to the adaptive kernel."""
+    waves per SIMD at 16 x 2, its momenta p0 = L z and M^-1 p0 from the
+    launch's pre-pass, nuts_dense_momenta_kernel) -- the same bits as the
+    oracle, partial wave included; a later warm-up run goes back to the
+    adaptive kernel. With the momentum pass off the sampling runs take the
+    adaptive kernel, which applies the metric itself: the same bits."""
     rng = np.random.default_rng(31)
     a = rng.standard_normal((D, D))
     cov = a @ a.T / D + 0.5 * np.eye(D)
     t = _gauss(gm, cov, rng.standard_normal(D))
     x0 = gm.init_with_seed(chains, D, 7, np.float64).astype(dtype)
     s, om = _check_run(gm, oracle, t, x0, dtype, 2, [(1, 60), (25, 0), (6, 20), (9, 0)], start_buffer=4,
-                       end_buffer=4, initial_window=10, layout=(16, 2))
+                       end_buffer=4, initial_window=10, layout=(16, 2), mpass=mpass)
     assert np.all(om.kind == 2)
-    assert s.launch_plan()["frozen"] == 1
+    assert s.launch_plan()["frozen"] == (1 if mpass else 0)
     s.run(2, 20)
     assert s.launch_plan()["frozen"] == 0
 
