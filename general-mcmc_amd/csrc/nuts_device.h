@@ -1015,6 +1015,8 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   // the launch's start records from the momentum pre-pass (a.zrec)
   const bool srec = (GM_SREC_DENSE || MASS != 3) && a.zmom != nullptr;
   // the frozen-dense kernel's momenta with the metric applied (a.pv0)
+  // (non-temporal loads of p0 / M^-1 p0 and stores of the samples measured
+  // -1.5 %, HBM 31.6 -> 29.0 GB: not kept, profiles/r06/ab_nuts_dense_prep2.log)
   // (known at compile time in the default build: no in-kernel draw, L
   // product or start-time M^-1 product is emitted there)
   const bool prepd = MASS == 3 && (GM_DENSE_PREP || a.pv0 != nullptr);

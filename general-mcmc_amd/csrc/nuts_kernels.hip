@@ -199,55 +199,61 @@ __global__ void nuts_momenta_kernel(uint64_t seed, uint32_t chain_offset, uint64
 // (M^-1 p)_i from +0 by fma, j ascending. The kernel's padded terms (j > i in
 // L, columns past D) add +-0 to a +0-started sum and change no bit, so they
 // are left out here. One block per chain: its L (transposed) and M^-1
-// (transposed, as the tree kernel's copy) staged in LDS once, then R = 256/D
-// transitions per round, thread (r, i) computing coordinate i of
-// transition s0 + r. Its LDS: nuts_dense_prep_lds (<= 64 KiB, else the tree
+// (transposed, as the tree kernel's copy) staged in LDS once, then
+// R = DPREP_THREADS / D transitions per round, thread (r, i) computing
+// coordinate i of transition s0 + r. Its LDS: nuts_dense_prep_lds (<= 64 KiB, else the tree
 // kernel applies the metric itself).
+constexpr int DPREP_THREADS = 1024;  // (cfg3_dense: 1.6 ms with 256 or 1024; 4.8 ms before the conflict-free [j][i] M^-1 view)
 static size_t nuts_dense_prep_lds(int D, size_t esz) {
   if (D < 1 || D > 256) return 0;
-  const size_t b = (2 * (size_t)D * D + (size_t)(256 / D) * D) * esz;
+  const size_t b = (2 * (size_t)D * D + 2 * (size_t)(DPREP_THREADS / D) * D) * esz;
   return b <= 64 * 1024 ? b : 0;
 }
 template <class T>
-__global__ __launch_bounds__(256) void nuts_dense_momenta_kernel(long long n, long long C, int D,
+__global__ __launch_bounds__(DPREP_THREADS) void nuts_dense_momenta_kernel(long long n, long long C, int D,
                                                                  const T* __restrict__ chol_rm,
                                                                  const T* __restrict__ minvT, T* __restrict__ pz,
                                                                  T* __restrict__ v0) {
   extern __shared__ __align__(16) unsigned char dm_lds[];
-  T* lt = (T*)dm_lds;       // [j][i] = L_ij
-  T* mt = lt + D * D;       // [j][i] = M^-1_ij
+  // [j][i] (lane i of a row reads consecutive words: no bank conflicts)
+  T* lt = (T*)dm_lds;       // L_ij
+  T* mt = lt + D * D;       // row i's entry j of the tree kernel's packed M^-1:
+                            // M^-1_ij while j <= i, M^-1_ji after (the same
+                            // values: M^-1 is exactly symmetric, and these are
+                            // the very words its product reads)
   T* zl = mt + D * D;       // [r][j] this round's normals, then momenta
   const long long c = blockIdx.x;
   const T* L = chol_rm + c * (long long)D * D;
-  const T* Mi = minvT + c * (long long)D * D;
+  const T* Mi = minvT + c * (long long)D * D;  // Mi[j*D + i] = M^-1_ij
   for (int k = threadIdx.x; k < D * D; k += blockDim.x) {
-    const int i = k / D, j = k - i * D;
-    lt[j * D + i] = L[k];  // L row-major: k = i*D + j
-    mt[k] = Mi[k];
+    const int j = k / D, i = k - j * D;
+    lt[k] = L[i * D + j];  // L row-major
+    mt[k] = j <= i ? Mi[k] : Mi[i * D + j];
   }
-  const int R = 256 / D;
+  const int R = DPREP_THREADS / D;
   const int r = threadIdx.x / D, i = threadIdx.x - r * D;
   const bool act = r < R;
+  T* pl = zl + R * D;  // [r][j] this round's momenta
+  // (the next round's normal loaded while this round's sums run; zl is
+  // rewritten only after every thread's reads of it, behind the second
+  // barrier of the previous round, and pl likewise behind the first)
+  T zn = (act && r < n) ? pz[((long long)r * C + c) * D + i] : (T)0;
   for (long long s0 = 0; s0 < n; s0 += R) {
     const long long s = s0 + r;
     const bool on = act && s < n;
     const long long o = (s * C + c) * D + i;
-    __syncthreads();  // (the previous round's reads of zl are done)
-    if (on) zl[r * D + i] = pz[o];
+    if (on) zl[r * D + i] = zn;
     __syncthreads();
+    if (act && s + R < n) zn = pz[o + (long long)R * C * D];
     T p = (T)0;
     if (on) {
       for (int j = 0; j <= i; ++j) p = p + lt[j * D + i] * zl[r * D + j];
+      pl[r * D + i] = p;
     }
     __syncthreads();
-    if (on) zl[r * D + i] = p;
-    __syncthreads();
     if (on) {
-      // the tree kernel's packed triangle: row i's entry j from M^-1_ij while
-      // j <= i, from M^-1_ji after (the same values: M^-1 is exactly
-      // symmetric, and this keeps the very same reads)
       T w = (T)0;
-      for (int j = 0; j < D; ++j) w = gfma(j <= i ? mt[j * D + i] : mt[i * D + j], zl[r * D + j], w);
+      for (int j = 0; j < D; ++j) w = gfma(mt[j * D + i], pl[r * D + j], w);
       pz[o] = p;
       v0[o] = w;
     }
@@ -683,10 +689,10 @@ int nuts_run(NutsState& ns, gm_dtype dt, const TargetDev& tg, const Layout& lay,
           if (dprep) {  // p0 = L z in place of z, M^-1 p0 at zvo
             void* pv = (char*)ns.zbuf + zvo;
             if (dt == GM_F32)
-              hipLaunchKernelGGL(nuts_dense_momenta_kernel<float>, dim3((unsigned)C), dim3(256), dpl, st, nst, C, D,
+              hipLaunchKernelGGL(nuts_dense_momenta_kernel<float>, dim3((unsigned)C), dim3(DPREP_THREADS), dpl, st, nst, C, D,
                                  (const float*)a.mchol_rm, (const float*)a.minv, (float*)ns.zbuf, (float*)pv);
             else
-              hipLaunchKernelGGL(nuts_dense_momenta_kernel<double>, dim3((unsigned)C), dim3(256), dpl, st, nst, C,
+              hipLaunchKernelGGL(nuts_dense_momenta_kernel<double>, dim3((unsigned)C), dim3(DPREP_THREADS), dpl, st, nst, C,
                                  D, (const double*)a.mchol_rm, (const double*)a.minv, (double*)ns.zbuf,
                                  (double*)pv);
             a.pv0 = pv;
