@@ -92,7 +92,8 @@ __device__ __forceinline__ void row_bcasts(const T (&p)[E], T (&pj)[NB]) {
 // rounds to -0 only when both are -0), so the padded columns change no bit.
 // (PB columns per batch: 8 at one wave per SIMD, 4 in the frozen-dense
 // kernel at two, where 8 cost 12 more spilled registers: measured 9.19e8 vs
-// 9.58e8 leapfrogs/s at cfg3_dense, profiles/r05/ab_dense_batches.log)
+// 9.58e8 leapfrogs/s at cfg3_dense, profiles/r05/ab_dense_batches.log; re-measured
+// after the round-6 start pre-pass: 8 still -2 %, ab_nuts_dense_l1reg_pb8.log)
 #ifndef GM_PACKED_BATCH
 #define GM_PACKED_BATCH 8
 #endif
@@ -722,9 +723,23 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   int l0n = 0, l0na = 0;
 #pragma unroll
   for (int e = 0; e < E; ++e) l0q[e] = l0p[e] = (T)0;
-  // (level 1 in registers as well, 12 more: the frozen-dense kernel spilled
-  // 60 registers and ran 5 % slower, cfg3's reached 256 and ran 13 % slower;
-  // profiles/r05/ab_dense_l1_registers.log, ab_cfg3_l1_registers.log)
+  // Level 1 in registers as well in the frozen-dense kernel (12 more, three
+  // vectors and the scalars): its stack levels are otherwise all in global
+  // memory, and level 1 is half of their traffic. With the start's products
+  // in the pre-pass the kernel spills 64 registers instead of 28 and runs
+  // 0.3-1.8 % faster (3 of 3 alternating rounds, 1.321e9 -> 1.334e9 median,
+  // profiles/r06/ab_nuts_dense_l1reg_pb8.log; before the pre-pass it spilled
+  // 60 and ran 5 % slower, profiles/r05/ab_dense_l1_registers.log)
+#ifndef GM_L1REG_FROZEN
+#define GM_L1REG_FROZEN 1
+#endif
+  constexpr bool L1R = GM_L1REG_FROZEN && MASS == 3 && L0REG;
+  T l1q[E], l1p[E], l1r[E], l1a = (T)0;
+  int l1n = 0, l1na = 0;
+#pragma unroll
+  for (int e = 0; e < E; ++e) l1q[e] = l1p[e] = l1r[e] = (T)0;
+  // (level 1 in registers in cfg3's identity kernel: it reached 256 and ran
+  // 13 % slower, profiles/r05/ab_cfg3_l1_registers.log)
   auto stack_store = [&](int k, const T (&f0)[E], const T (&f1)[E], const T (&f2)[E], T al, int nn,
                          int nna) __attribute__((always_inline)) {
     if (L0REG && k == 0) {
@@ -736,6 +751,16 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       l0a = al;
       l0n = nn;
       l0na = nna;
+    } else if (L1R && k == 1) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        l1q[e] = f0[e];
+        l1p[e] = f1[e];
+        l1r[e] = f2[e];
+      }
+      l1a = al;
+      l1n = nn;
+      l1na = nna;
     } else if (k < KL) {
       T* v = lvec + (long long)k * 3 * NT * E + tix * E;
 #pragma unroll
@@ -769,6 +794,9 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
     if (L0REG && k == 0) {
 #pragma unroll
       for (int e = 0; e < E; ++e) out[e] = f == 1 ? l0p[e] : l0q[e];
+    } else if (L1R && k == 1) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) out[e] = f == 0 ? l1q[e] : f == 1 ? l1p[e] : l1r[e];
     } else if (k < KL) {
       const T* v = lvec + ((long long)k * 3 + f) * NT * E + tix * E;
 #pragma unroll
@@ -786,7 +814,7 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   // registers and LDS are read by every lane (in bounds, and an LDS read costs
   // no more for the lanes that discard it), HBM only by the lanes of pred
   auto stack_vec_if = [&](int k, int f, T (&out)[E], bool pred) __attribute__((always_inline)) {
-    if ((L0REG && k == 0) || k < KL) {
+    if ((L0REG && k == 0) || (L1R && k == 1) || k < KL) {
       stack_vec(k, f, out);
     } else {
       const T* sv = (const T*)(sbase + k * a.stk_es) + f * D;
@@ -802,6 +830,10 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
       al = l0a;
       nn = l0n;
       nna = l0na;
+    } else if (L1R && k == 1) {
+      al = l1a;
+      nn = l1n;
+      nna = l1na;
     } else if (k < KL) {
       al = lalpha[k * CPB + cib];
       nn = lnn[k * CPB + cib];
