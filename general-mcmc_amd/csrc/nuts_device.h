@@ -729,7 +729,9 @@ void nuts_kernel(NutsLaunch a, TG tg_) {
   // in the pre-pass the kernel spills 64 registers instead of 28 and runs
   // 0.3-1.8 % faster (3 of 3 alternating rounds, 1.321e9 -> 1.334e9 median,
   // profiles/r06/ab_nuts_dense_l1reg_pb8.log; before the pre-pass it spilled
-  // 60 and ran 5 % slower, profiles/r05/ab_dense_l1_registers.log)
+  // 60 and ran 5 % slower, profiles/r05/ab_dense_l1_registers.log). Level 2
+  // in registers too: 63 spills, -7 % (1.332e9 -> 1.236e9 median of 4,
+  // profiles/r06/ab_nuts_dense_l2reg.log).
 #ifndef GM_L1REG_FROZEN
 #define GM_L1REG_FROZEN 1
 #endif
