@@ -254,7 +254,8 @@ int gm_nuts_set_dense_forms(gm_sampler* s, int32_t minv_lds, int32_t chol_lds);
  * plan[1] M^-1 form (0 global, 1 packed, 2 full), plan[2] its LDS offset,
  * plan[3] Cholesky factor in LDS (0/1), plan[4] its offset, plan[5] 1 when
  * the launch ran the frozen-dense kernel (every chain's metric dense, no
- * warm-up window: GM_FROZEN_WAVES waves per SIMD). The first min(cap, 6)
+ * warm-up window, the momentum pass on: GM_FROZEN_WAVES waves per SIMD).
+ * The first min(cap, 6)
  * values are written to plan (cap >= 1); returns GM_OK. */
 int gm_nuts_get_plan(gm_sampler* s, int32_t* plan, int32_t cap);
 
@@ -263,8 +264,11 @@ int gm_nuts_get_plan(gm_sampler* s, int32_t* plan, int32_t cap);
  * the sampler keeps for its later launches (at most 4 GiB and a quarter of
  * the device memory free when it grows; a launch it does not fit draws in the
  * kernel), off in the tree kernel at each transition start (switching it off
- * releases the buffer). The same Philox/Box-Muller values either way
- * (identical results); no reference counterpart. */
+ * releases the buffer). With a dense metric the pass also applies it (the
+ * momenta L z and their M^-1 L z, in a second [steps][C][D] buffer) for the
+ * frozen-dense kernel, which needs it: with the pass off those launches run
+ * the adaptive dense kernel. The same Philox/Box-Muller values and the same
+ * sums either way (identical results); no reference counterpart. */
 int gm_nuts_set_momentum_pass(gm_sampler* s, int32_t on);
 
 int gm_nuts_get_mass(gm_sampler* s, int32_t* mode, int32_t* kind, void* dinv, void* dsqrt, void* minv,
